@@ -1,0 +1,120 @@
+"""ctypes binding of libarx.so (include/arx.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load,
+every entry point raises ArxError immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ARX_LIB", os.path.join(_PKG, "libarx.so"))
+
+ARX_OK = 0
+STATUS_NAMES = {
+    0: "ARX_OK", 1: "ARX_ERR_INVALID_ARGUMENT", 2: "ARX_ERR_HIP", 3: "ARX_ERR_OUT_OF_MEMORY",
+    4: "ARX_ERR_NOT_READY", 5: "ARX_ERR_IO", 6: "ARX_ERR_INTERNAL",
+}
+
+
+class ArxError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+class ArxConfig(C.Structure):
+    _fields_ = [
+        ("rays_x", C.c_int32), ("rays_y", C.c_int32), ("rays_z", C.c_int32),
+        ("ir_length_in_seconds", C.c_uint32), ("sample_rate", C.c_int32),
+        ("base_power", C.c_float), ("energy_thres", C.c_float), ("max_bounces", C.c_uint32),
+        ("hrtf_absorption_rate", C.c_float), ("is_mono", C.c_int32), ("seed", C.c_uint64),
+        ("device", C.c_int32),
+    ]
+
+
+class ArxStats(C.Structure):
+    _fields_ = [
+        ("queries", C.c_uint64), ("receiver_hits", C.c_uint64), ("misses", C.c_uint64),
+        ("trace_ms", C.c_double), ("conv_ms", C.c_double),
+        ("n_scene_tris", C.c_int64), ("n_receiver_tris", C.c_int64), ("n_nodes", C.c_int64),
+        ("bvh_depth", C.c_int32),
+    ]
+
+
+_P = C.c_void_p
+_F = C.POINTER(C.c_float)
+_D = C.POINTER(C.c_double)
+
+# name -> (restype, argtypes); must cover every function declared in include/arx.h
+SIGNATURES = {
+    "arx_status_string": (C.c_char_p, [C.c_int]),
+    "arx_last_error": (C.c_char_p, []),
+    "arx_abi_version": (C.c_int, []),
+    "arx_default_config": (None, [C.POINTER(ArxConfig)]),
+    "arx_create": (C.c_int, [C.POINTER(ArxConfig), C.POINTER(_P)]),
+    "arx_destroy": (None, [_P]),
+    "arx_get_config": (C.c_int, [_P, C.POINTER(ArxConfig)]),
+    "arx_set_stream": (C.c_int, [_P, _P]),
+    "arx_get_stream": (_P, [_P]),
+    "arx_set_scene": (C.c_int, [_P, _F, _F, C.c_int64]),
+    "arx_set_receiver_model": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
+    "arx_place_receiver_vertices": (C.c_int, [_F, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, _F]),
+    "arx_material_absorption": (C.c_float, [C.c_char_p, C.POINTER(C.c_char_p), _F, C.c_size_t]),
+    "arx_set_emitter": (C.c_int, [_P, C.c_float, C.c_float, C.c_float]),
+    "arx_set_listener": (C.c_int, [_P, C.c_float, C.c_float, C.c_float, C.c_float]),
+    "arx_set_thresholds": (C.c_int, [_P, C.c_float, C.c_uint32]),
+    "arx_set_hrtf_absorption_rate": (C.c_int, [_P, C.c_float]),
+    "arx_set_base_power": (C.c_int, [_P, C.c_float]),
+    "arx_set_mono_output": (C.c_int, [_P, C.c_int]),
+    "arx_set_seed": (C.c_int, [_P, C.c_uint64]),
+    "arx_render": (C.c_int, [_P, _D]),
+    "arx_clear_histogram": (C.c_int, [_P]),
+    "arx_trace_rays": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
+    "arx_histogram_device": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t)]),
+    "arx_finalize_ir": (C.c_int, [_P]),
+    "arx_attach_histogram": (C.c_int, [_P, _P, C.c_size_t]),
+    "arx_ir_device": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_size_t)]),
+    "arx_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
+    "arx_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),
+    "arx_frac_bits": (C.c_int, [C.c_uint64]),
+    "arx_set_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
+    "arx_convolute_audio_file": (C.c_int, [_P, _F, C.c_size_t, _F, _F, _D, _D]),
+    "arx_convolute_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> C.CDLL:
+    """Load libarx.so once; raise (never fall back) if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ArxError(5, f"{LIB_PATH} not built: run `python -m audiorenderingv2_amd.build` "
+                                  "(there is no CPU fallback for the HIP path)")
+            handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            if handle.arx_abi_version() != 1:
+                raise ArxError(6, "ABI version mismatch")
+            _lib = handle
+        return _lib
+
+
+def check(status: int) -> None:
+    if status != ARX_OK:
+        msg = lib().arx_last_error().decode(errors="replace")
+        raise ArxError(status, msg)
+
+
+def fptr(a) -> "C._Pointer":
+    """float32 numpy array -> POINTER(c_float) (no copy)."""
+    return a.ctypes.data_as(_F)

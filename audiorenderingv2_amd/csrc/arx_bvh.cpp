@@ -1,0 +1,228 @@
+// arx_bvh.cpp -- binned-SAH BVH2 builder for the trace kernel's 64-B node layout.
+//
+// The reference builds an OptiX GAS over per-material meshes (AudioRenderer.cpp:95-218);
+// here the static scene is built once and the receiver halves get their own small
+// sub-tree (rebuilt per listener move in microseconds).  Boxes are padded by
+// 1e-5 * max|coordinate| so that box rejection is conservative w.r.t. the watertight
+// triangle test: the BVH closest hit is exactly the brute-force closest hit.
+#include "arx_bvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace arx {
+namespace {
+
+constexpr int kBins = 32;
+constexpr int kLeafMax = 4;          // SAH may stop at <= kLeafMax
+constexpr float kTraversalCost = 1.0f;
+constexpr float kIntersectCost = 1.0f;
+
+struct Prim {
+    float lo[3], hi[3], c[3];
+    int32_t idx;
+};
+
+struct Box {
+    float lo[3] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
+                   std::numeric_limits<float>::max()};
+    float hi[3] = {-std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(),
+                   -std::numeric_limits<float>::max()};
+    void grow(const float* l, const float* h) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], l[k]);
+            hi[k] = std::max(hi[k], h[k]);
+        }
+    }
+    void grow_pt(const float* p) { grow(p, p); }
+    bool empty() const { return lo[0] > hi[0]; }
+    float area() const {
+        if (empty()) return 0.0f;
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct Builder {
+    std::vector<Prim> prims;
+    BvhBuild* out;
+    const float* tri_v;
+    const float* tri_abs;
+    float abs_fill;
+    int32_t id_base;
+    float pad;
+
+    ChildRef make_ref(const Box& b, int32_t ref, int32_t count) const {
+        ChildRef c;
+        for (int k = 0; k < 3; ++k) {
+            c.lo[k] = b.lo[k] - pad;
+            c.hi[k] = b.hi[k] + pad;
+        }
+        c.ref = ref;
+        c.count = count;
+        return c;
+    }
+
+    ChildRef leaf(int64_t begin, int64_t end, const Box& b) {
+        int32_t first = (int32_t)out->tris.size();
+        for (int64_t i = begin; i < end; ++i) {
+            int32_t src = prims[i].idx;
+            TriRec t;
+            std::memset(&t, 0, sizeof(t));
+            const float* v = tri_v + 9 * (int64_t)src;
+            for (int k = 0; k < 3; ++k) {
+                t.v0[k] = v[k];
+                t.v1[k] = v[3 + k];
+                t.v2[k] = v[6 + k];
+            }
+            t.absorption = tri_abs ? tri_abs[src] : abs_fill;
+            t.id = id_base + src;
+            out->tris.push_back(t);
+        }
+        return make_ref(b, first, (int32_t)(end - begin));
+    }
+
+    ChildRef build(int64_t begin, int64_t end, int depth) {
+        Box bounds, cbounds;
+        for (int64_t i = begin; i < end; ++i) {
+            bounds.grow(prims[i].lo, prims[i].hi);
+            cbounds.grow_pt(prims[i].c);
+        }
+        const int64_t n = end - begin;
+        out->depth = std::max(out->depth, depth);
+        if (n <= 1 || depth >= kMaxBuildDepth) return leaf(begin, end, bounds);
+
+        // binned SAH over centroids
+        int best_axis = -1, best_split = -1;
+        float best_cost = std::numeric_limits<float>::max();
+        for (int axis = 0; axis < 3; ++axis) {
+            float cmin = cbounds.lo[axis], cmax = cbounds.hi[axis];
+            if (!(cmax > cmin)) continue;
+            float scale = kBins / (cmax - cmin);
+            Box bb[kBins];
+            int64_t cnt[kBins] = {0};
+            for (int64_t i = begin; i < end; ++i) {
+                int b = std::min(kBins - 1, (int)((prims[i].c[axis] - cmin) * scale));
+                cnt[b]++;
+                bb[b].grow(prims[i].lo, prims[i].hi);
+            }
+            float right_area[kBins];
+            int64_t right_cnt[kBins];
+            Box acc;
+            int64_t ac = 0;
+            for (int b = kBins - 1; b > 0; --b) {
+                acc.grow(bb[b].lo, bb[b].hi);
+                ac += cnt[b];
+                right_area[b] = acc.area();
+                right_cnt[b] = ac;
+            }
+            Box lacc;
+            int64_t lc = 0;
+            for (int b = 0; b < kBins - 1; ++b) {
+                lacc.grow(bb[b].lo, bb[b].hi);
+                lc += cnt[b];
+                if (lc == 0 || right_cnt[b + 1] == 0) continue;
+                float cost = lacc.area() * (float)lc + right_area[b + 1] * (float)right_cnt[b + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_split = b;
+                }
+            }
+        }
+        float parent_area = bounds.area();
+        float sah = kTraversalCost + (parent_area > 0 ? kIntersectCost * best_cost / parent_area : 0.0f);
+        if (n <= kLeafMax && (best_axis < 0 || sah >= kIntersectCost * (float)n)) return leaf(begin, end, bounds);
+
+        int64_t mid;
+        if (best_axis >= 0) {
+            float cmin = cbounds.lo[best_axis], cmax = cbounds.hi[best_axis];
+            float scale = kBins / (cmax - cmin);
+            auto it = std::stable_partition(prims.begin() + begin, prims.begin() + end, [&](const Prim& p) {
+                int b = std::min(kBins - 1, (int)((p.c[best_axis] - cmin) * scale));
+                return b <= best_split;
+            });
+            mid = it - prims.begin();
+        } else {
+            mid = begin + n / 2;  // all centroids coincide: split by position in the list
+        }
+        if (mid == begin || mid == end) mid = begin + n / 2;
+
+        int32_t me = (int32_t)out->nodes.size();
+        out->nodes.emplace_back();
+        ChildRef l = build(begin, mid, depth + 1);
+        ChildRef r = build(mid, end, depth + 1);
+        out->nodes[me] = make_node(l, r);
+        ChildRef self = make_ref(bounds, me, 0);
+        return self;
+    }
+};
+
+}  // namespace
+
+ChildRef empty_child() {
+    ChildRef c;
+    for (int k = 0; k < 3; ++k) {
+        c.lo[k] = 1e30f;
+        c.hi[k] = -1e30f;
+    }
+    c.ref = 0;
+    c.count = 0;  // never traversed: the inverted box rejects every ray
+    return c;
+}
+
+BvhNode make_node(const ChildRef& c0, const ChildRef& c1) {
+    BvhNode n;
+    n.a[0] = c0.lo[0]; n.a[1] = c0.hi[0]; n.a[2] = c0.lo[1]; n.a[3] = c0.hi[1];
+    n.b[0] = c1.lo[0]; n.b[1] = c1.hi[0]; n.b[2] = c1.lo[1]; n.b[3] = c1.hi[1];
+    n.c[0] = c0.lo[2]; n.c[1] = c0.hi[2]; n.c[2] = c1.lo[2]; n.c[3] = c1.hi[2];
+    n.d[0] = c0.ref; n.d[1] = c1.ref; n.d[2] = c0.count; n.d[3] = c1.count;
+    return n;
+}
+
+void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, int64_t n, int32_t id_base,
+               BvhBuild& out) {
+    out.nodes.clear();
+    out.tris.clear();
+    out.depth = 0;
+    if (n <= 0) {
+        out.root = empty_child();
+        return;
+    }
+    Builder b;
+    b.out = &out;
+    b.tri_v = tri_v;
+    b.tri_abs = tri_abs;
+    b.abs_fill = absorption_fill;
+    b.id_base = id_base;
+    float mx = 0.0f;
+    b.prims.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        Prim& p = b.prims[i];
+        const float* v = tri_v + 9 * i;
+        for (int k = 0; k < 3; ++k) {
+            p.lo[k] = std::min(v[k], std::min(v[3 + k], v[6 + k]));
+            p.hi[k] = std::max(v[k], std::max(v[3 + k], v[6 + k]));
+            p.c[k] = 0.5f * (p.lo[k] + p.hi[k]);
+            mx = std::max(mx, std::max(std::fabs(p.lo[k]), std::fabs(p.hi[k])));
+        }
+        p.idx = (int32_t)i;
+    }
+    b.pad = std::max(1e-5f * mx, 1e-6f);
+    out.nodes.reserve((size_t)(2 * n / kLeafMax + 16));
+    out.tris.reserve((size_t)n);
+    out.root = b.build(0, n, 1);
+}
+
+void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset) {
+    auto fix = [&](int32_t& ref, int32_t count) { ref += (count > 0) ? tri_offset : node_offset; };
+    for (BvhNode& n : b.nodes) {
+        fix(n.d[0], n.d[2]);
+        fix(n.d[1], n.d[3]);
+    }
+    if (!(b.root.count == 0 && b.root.lo[0] > b.root.hi[0])) fix(b.root.ref, b.root.count);
+}
+
+}  // namespace arx

@@ -1,0 +1,33 @@
+// arx_bvh.hpp -- host-side SAH BVH builder (replaces optixAccelBuild/optixAccelCompact,
+// R/prebuild/obj_raytracer/AudioRenderer.cpp:179-208).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "arx_layout.hpp"
+
+namespace arx {
+
+struct ChildRef {
+    float lo[3], hi[3];  // padded box
+    int32_t ref;         // inner: node index; leaf: first triangle
+    int32_t count;       // 0 = inner node
+};
+
+struct BvhBuild {
+    std::vector<BvhNode> nodes;  // indices local to this build
+    std::vector<TriRec> tris;    // leaf order, indices local to this build
+    ChildRef root;
+    int depth = 0;
+};
+
+// tri_v: n*9 floats, tri_abs: n floats (may be nullptr -> absorption_fill).
+void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, int64_t n, int32_t id_base,
+               BvhBuild& out);
+// Shift all node / triangle references by the given offsets (placing the build inside a
+// bigger array).  The root reference is shifted too.
+void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
+BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
+ChildRef empty_child();
+
+}  // namespace arx

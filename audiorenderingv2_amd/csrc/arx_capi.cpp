@@ -1,0 +1,633 @@
+// arx_capi.cpp -- C ABI of libarx.so (include/arx.h): renderer state, scene upload,
+// listener placement and the render / convolution entry points.
+//
+// Host-side counterpart of R/prebuild/obj_raytracer/AudioRenderer.cpp (OptiX setup,
+// buildAccel, buildSBT, reload, render, convoluteAudioFile), re-designed for HIP:
+// one stream per renderer, persistent device buffers (the reference cudaMallocs and
+// frees inside every call, AudioRenderer.cpp:593-750), status codes instead of
+// throw/exit, and no full rebuild when the listener moves.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/arx.h"
+#include "arx_bvh.hpp"
+#include "arx_kernels.hpp"
+#include "arx_layout.hpp"
+
+using namespace arx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+arx_status fail(arx_status s, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return s;
+}
+
+#define ARX_HIP(call)                                                                                      \
+    do {                                                                                                   \
+        hipError_t e_ = (call);                                                                            \
+        if (e_ != hipSuccess)                                                                              \
+            return fail(e_ == hipErrorOutOfMemory ? ARX_ERR_OUT_OF_MEMORY : ARX_ERR_HIP, "%s failed: %s (%s:%d)", \
+                        #call, hipGetErrorString(e_), __FILE__, __LINE__);                                 \
+    } while (0)
+
+}  // namespace
+
+struct arx_renderer {
+    arx_config cfg;
+    int32_t ir_len = 0;
+    int cus = 256;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    float emitter[3] = {0.f, 0.f, 0.f};
+    float center[3] = {0.f, 0.f, 0.f};
+    float yaw = 0.f;
+
+    // host scene
+    int64_t n_scene = 0;
+    BvhBuild scene;
+    std::vector<float> recv_local[2];
+    BvhBuild recv;
+    bool scene_dirty = true;
+    bool recv_dirty = true;
+    bool scene_set = false;
+
+    // device
+    BvhNode* d_nodes = nullptr;
+    size_t nodes_cap = 0;
+    TriRec* d_tris = nullptr;
+    size_t tris_cap = 0;
+    unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
+    unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
+    unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
+    float* d_ir = nullptr;                 // 2*ir_len: L then R
+    unsigned long long* d_counters = nullptr;
+    unsigned long long* h_counters = nullptr;  // pinned
+
+    ConvPlan* conv = nullptr;
+    bool conv_ir_dirty = true;
+    float* d_conv_in = nullptr;
+    float* d_conv_out = nullptr;
+    size_t conv_cap = 0;
+
+    arx_stats stats;
+};
+
+namespace {
+
+uint64_t n_rays(const arx_config& c) {
+    return (uint64_t)(int64_t)c.rays_x * (uint64_t)(int64_t)c.rays_y * (uint64_t)(int64_t)c.rays_z;
+}
+
+float initial_energy(const arx_config& c) {
+    // devicePrograms.cu:208 -- (x*y*z) is an int product in the reference
+    const int32_t n = c.rays_x * c.rays_y * c.rays_z;
+    return (float)((double)c.base_power / ((double)n * 4.18879020478));
+}
+
+arx_status check_config(const arx_config* c) {
+    if (!c) return fail(ARX_ERR_INVALID_ARGUMENT, "config is NULL");
+    if (c->rays_x <= 0 || c->rays_y <= 0 || c->rays_z <= 0)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "rays dims must be positive");
+    if ((uint64_t)c->rays_x * (uint64_t)c->rays_y * (uint64_t)c->rays_z > 0x7fffffffull)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "x*y*z must fit int32 (devicePrograms.cu:208 int product)");
+    if (c->sample_rate <= 0) return fail(ARX_ERR_INVALID_ARGUMENT, "sample_rate must be positive");
+    if (c->ir_length_in_seconds == 0) return fail(ARX_ERR_INVALID_ARGUMENT, "ir_length_in_seconds must be >= 1");
+    const uint64_t L = (uint64_t)c->ir_length_in_seconds * (uint64_t)c->sample_rate;
+    if (L > 0x7fffffffull) return fail(ARX_ERR_INVALID_ARGUMENT, "ir length too large");
+    return ARX_OK;
+}
+
+// OptixModel.cpp:178-193 (glm::rotate(mat4(1), -radians(yaw), +Y) * v, then + camera),
+// restated with glm's exact operation order (matrix_transform.inl rotate, type_mat4x4.inl
+// operator*): x' = (c*x + R10*y) + (s*z + 0), y' = (0*x + R11*y) + (0*z + 0),
+// z' = (-s*x + 0*y) + (c*z + 0) with c = cos(-a), s = sin(-a), R11 = c + (1 - c).
+void place_vertices(const float* local, int64_t n_vertices, float x, float y, float z, float yaw_deg, float* out) {
+    const float ang = yaw_deg * static_cast<float>(0.01745329251994329576923690768489);  // glm::radians
+    const float a = -ang;
+    const float c = std::cos(a);
+    const float s = std::sin(a);
+    const float t1 = 1.0f - c;   // temp = (1 - c) * axis, axis = (0, 1, 0)
+    const float r00 = c + 0.0f * 0.0f;
+    const float r10 = t1 * 0.0f - s * 0.0f;
+    const float r20 = 0.0f * 0.0f + s * 1.0f;
+    const float r01 = 0.0f * 1.0f + s * 0.0f;
+    const float r11 = c + t1 * 1.0f;
+    const float r21 = 0.0f * 1.0f - s * 0.0f;
+    const float r02 = 0.0f * 0.0f - s * 1.0f;
+    const float r12 = t1 * 0.0f + s * 0.0f;
+    const float r22 = c + 0.0f * 0.0f;
+    for (int64_t i = 0; i < n_vertices; ++i) {
+        const float vx = local[3 * i + 0], vy = local[3 * i + 1], vz = local[3 * i + 2];
+        const float ox = (r00 * vx + r10 * vy) + (r20 * vz + 0.0f * 1.0f);
+        const float oy = (r01 * vx + r11 * vy) + (r21 * vz + 0.0f * 1.0f);
+        const float oz = (r02 * vx + r12 * vy) + (r22 * vz + 0.0f * 1.0f);
+        out[3 * i + 0] = x + ox;
+        out[3 * i + 1] = y + oy;
+        out[3 * i + 2] = z + oz;
+    }
+}
+
+arx_status ensure_device_scene(arx_renderer* r) {
+    if (!r->scene_set) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
+    if (r->recv_dirty) {
+        // receiver halves placed in world space, left then right (placeReceiver OptixModel.cpp:153-157)
+        std::vector<float> tv;
+        std::vector<float> ab;
+        for (int side = 0; side < 2; ++side) {
+            const std::vector<float>& loc = r->recv_local[side];
+            const int64_t nt = (int64_t)loc.size() / 9;
+            size_t base = tv.size();
+            tv.resize(base + loc.size());
+            place_vertices(loc.data(), 3 * nt, r->center[0], r->center[1], r->center[2], r->yaw, tv.data() + base);
+            ab.insert(ab.end(), (size_t)nt, side == 0 ? -1.0f : -2.0f);
+        }
+        build_bvh(tv.data(), ab.data(), 0.0f, (int64_t)ab.size(), (int32_t)r->n_scene, r->recv);
+        relocate_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), (int32_t)r->scene.tris.size());
+    }
+    const size_t n_nodes = 1 + r->scene.nodes.size() + r->recv.nodes.size();
+    const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
+    bool full = r->scene_dirty;
+    if (n_nodes > r->nodes_cap) {
+        if (r->d_nodes) ARX_HIP(hipFree(r->d_nodes));
+        r->d_nodes = nullptr;
+        size_t cap = n_nodes + 1024;
+        ARX_HIP(hipMalloc(&r->d_nodes, cap * sizeof(BvhNode)));
+        r->nodes_cap = cap;
+        full = true;
+    }
+    if (n_tris > r->tris_cap || r->d_tris == nullptr) {
+        if (r->d_tris) ARX_HIP(hipFree(r->d_tris));
+        r->d_tris = nullptr;
+        size_t cap = std::max<size_t>(n_tris + 4096, 1);
+        ARX_HIP(hipMalloc(&r->d_tris, cap * sizeof(TriRec)));
+        r->tris_cap = cap;
+        full = true;
+    }
+    if (full || r->recv_dirty) {
+        BvhNode top = make_node(r->scene.root, r->recv.root);
+        ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+        if (full && !r->scene.nodes.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(), r->scene.nodes.size() * sizeof(BvhNode),
+                                   hipMemcpyHostToDevice, r->stream));
+        if (full && !r->scene.tris.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
+                                   hipMemcpyHostToDevice, r->stream));
+        if (!r->recv.nodes.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_nodes + 1 + r->scene.nodes.size(), r->recv.nodes.data(),
+                                   r->recv.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+        if (!r->recv.tris.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
+                                   r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
+        // the host vectors are pageable: make sure the copies are done before they can change
+        ARX_HIP(hipStreamSynchronize(r->stream));
+    }
+    r->scene_dirty = false;
+    r->recv_dirty = false;
+    r->stats.n_scene_tris = r->n_scene;
+    r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
+    r->stats.n_nodes = (int64_t)n_nodes;
+    r->stats.bvh_depth = 1 + std::max(r->scene.depth, r->recv.depth);
+    return ARX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* arx_status_string(arx_status s) {
+    switch (s) {
+        case ARX_OK: return "ok";
+        case ARX_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case ARX_ERR_HIP: return "HIP error";
+        case ARX_ERR_OUT_OF_MEMORY: return "out of memory";
+        case ARX_ERR_NOT_READY: return "not ready";
+        case ARX_ERR_IO: return "I/O error";
+        case ARX_ERR_INTERNAL: return "internal error";
+    }
+    return "unknown status";
+}
+
+const char* arx_last_error(void) { return g_last_error.c_str(); }
+
+int arx_abi_version(void) { return ARX_ABI_VERSION; }
+
+int arx_frac_bits(uint64_t n) {
+    int lg = 0;
+    while (((uint64_t)1 << lg) < n && lg < 63) ++lg;
+    int fb = 59 - lg;
+    return std::min(52, std::max(8, fb));
+}
+
+void arx_default_config(arx_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->rays_x = c->rays_y = c->rays_z = 100;  // Context.cpp:114
+    c->ir_length_in_seconds = 2;              // :21
+    c->sample_rate = 44100;                   // live-mode default (:221)
+    c->base_power = 100.0f;                   // :113
+    c->energy_thres = 0.0f;                   // :115
+    c->max_bounces = 10;                      // :116
+    c->hrtf_absorption_rate = 1.0f;           // round(0.9) (:117, :145)
+    c->is_mono = 0;
+    c->seed = 1;
+    c->device = 0;
+}
+
+float arx_material_absorption(const char* name, const char* const* names, const float* absorption, size_t n) {
+    if (!name) return 0.5f;
+    if (std::strcmp(name, "receiver_left") == 0) return -1.0f;
+    if (std::strcmp(name, "receiver_right") == 0) return -2.0f;
+    for (size_t i = 0; i < n; ++i)
+        if (names && names[i] && std::strcmp(names[i], name) == 0) return absorption[i];
+    return 0.5f;
+}
+
+arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
+    if (!out) return fail(ARX_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    arx_status st = check_config(cfg);
+    if (st != ARX_OK) return st;
+    int ndev = 0;
+    ARX_HIP(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "device %d out of range (%d devices)", cfg->device, ndev);
+    ARX_HIP(hipSetDevice(cfg->device));
+    arx_renderer* r = new (std::nothrow) arx_renderer();
+    if (!r) return fail(ARX_ERR_OUT_OF_MEMORY, "host allocation failed");
+    std::memset(&r->stats, 0, sizeof(r->stats));
+    r->cfg = *cfg;
+    r->ir_len = (int32_t)(cfg->ir_length_in_seconds * (uint32_t)cfg->sample_rate);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess) r->cus = prop.multiProcessorCount;
+    auto cleanup = [&](arx_status s) {
+        arx_destroy(r);
+        return s;
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&r->ev0)) != hipSuccess || (e = hipEventCreate(&r->ev1)) != hipSuccess ||
+        (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc(&r->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc(&r->h_counters, 8 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
+        return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
+    r->stream = r->own_stream;
+    if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(r->stream)) != hipSuccess)
+        return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
+    *out = r;
+    return ARX_OK;
+}
+
+void arx_destroy(arx_renderer* r) {
+    if (!r) return;
+    hipSetDevice(r->cfg.device);
+    if (r->stream) hipStreamSynchronize(r->stream);
+    if (r->conv) conv_plan_destroy(r->conv);
+    hipFree(r->d_nodes);
+    hipFree(r->d_tris);
+    hipFree(r->d_hist);
+    hipFree(r->d_ir);
+    hipFree(r->d_counters);
+    hipFree(r->d_conv_in);
+    hipFree(r->d_conv_out);
+    if (r->h_counters) hipHostFree(r->h_counters);
+    if (r->ev0) hipEventDestroy(r->ev0);
+    if (r->ev1) hipEventDestroy(r->ev1);
+    if (r->own_stream) hipStreamDestroy(r->own_stream);
+    delete r;
+}
+
+arx_status arx_get_config(const arx_renderer* r, arx_config* out) {
+    if (!r || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out = r->cfg;
+    return ARX_OK;
+}
+
+arx_status arx_set_stream(arx_renderer* r, void* s) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->stream = s ? (hipStream_t)s : r->own_stream;
+    return ARX_OK;
+}
+
+void* arx_get_stream(const arx_renderer* r) { return r ? (void*)r->stream : nullptr; }
+
+arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_abs, int64_t n) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n < 0 || (n > 0 && (!tri_v || !tri_abs))) return fail(ARX_ERR_INVALID_ARGUMENT, "bad scene arrays");
+    if (n > (int64_t)0x3fffffff) return fail(ARX_ERR_INVALID_ARGUMENT, "too many triangles");
+    for (int64_t i = 0; i < 9 * n; ++i)
+        if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
+    build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
+    relocate_bvh(r->scene, 1, 0);
+    r->n_scene = n;
+    r->scene_set = true;
+    r->scene_dirty = true;
+    r->recv_dirty = true;  // receiver ids and offsets follow the scene
+    return ARX_OK;
+}
+
+arx_status arx_set_receiver_model(arx_renderer* r, int side, const float* tri_v, int64_t n) {
+    if (!r || side < 0 || side > 1 || n < 0 || (n > 0 && !tri_v))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad receiver model arguments");
+    r->recv_local[side].assign(tri_v, tri_v + 9 * n);
+    r->recv_dirty = true;
+    return ARX_OK;
+}
+
+arx_status arx_place_receiver_vertices(const float* local_xyz, int64_t n_vertices, float x, float y, float z,
+                                       float yaw_deg, float* out_xyz) {
+    if (n_vertices < 0 || (n_vertices > 0 && (!local_xyz || !out_xyz)))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    place_vertices(local_xyz, n_vertices, x, y, z, yaw_deg, out_xyz);
+    return ARX_OK;
+}
+
+arx_status arx_set_emitter(arx_renderer* r, float x, float y, float z) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->emitter[0] = x;
+    r->emitter[1] = y;
+    r->emitter[2] = z;
+    return ARX_OK;
+}
+
+arx_status arx_set_listener(arx_renderer* r, float x, float y, float z, float yaw_deg) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->center[0] = x;
+    r->center[1] = y;
+    r->center[2] = z;
+    r->yaw = yaw_deg;
+    r->recv_dirty = true;
+    return ARX_OK;
+}
+
+arx_status arx_set_thresholds(arx_renderer* r, float energy, uint32_t max_bounces) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->cfg.energy_thres = energy;
+    r->cfg.max_bounces = max_bounces;
+    return ARX_OK;
+}
+
+arx_status arx_set_hrtf_absorption_rate(arx_renderer* r, float v) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->cfg.hrtf_absorption_rate = v;
+    return ARX_OK;
+}
+
+arx_status arx_set_base_power(arx_renderer* r, float v) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->cfg.base_power = v;
+    return ARX_OK;
+}
+
+arx_status arx_set_mono_output(arx_renderer* r, int mono) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->cfg.is_mono = mono ? 1 : 0;
+    return ARX_OK;
+}
+
+arx_status arx_set_seed(arx_renderer* r, uint64_t seed) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->cfg.seed = seed;
+    return ARX_OK;
+}
+
+arx_status arx_clear_histogram(arx_renderer* r) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipMemsetAsync(r->hist(), 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream));
+    ARX_HIP(hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (ray_end < ray_begin) return fail(ARX_ERR_INVALID_ARGUMENT, "ray_end < ray_begin");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = ensure_device_scene(r);
+    if (st != ARX_OK) return st;
+    const arx_config& c = r->cfg;
+    TraceArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.nodes = r->d_nodes;
+    a.tris = r->d_tris;
+    a.hist = r->hist();
+    a.counters = r->d_counters;
+    a.seed = c.seed;
+    a.ray_begin = ray_begin;
+    a.ray_end = ray_end;
+    for (int k = 0; k < 3; ++k) {
+        a.emitter[k] = r->emitter[k];
+        a.center[k] = r->center[k];
+    }
+    a.e0 = initial_energy(c);
+    a.inv_unit = (a.e0 != 0.0f) ? std::ldexp(1.0, arx_frac_bits(n_rays(c))) / (double)a.e0 : 0.0;
+    a.energy_thres = c.energy_thres;
+    a.hrtf = c.hrtf_absorption_rate;
+    int32_t secs = r->ir_len / c.sample_rate;  // devicePrograms.cu:227-228
+    secs = std::max(1, std::min(secs, 999));
+    a.dist_limit = (float)(secs * kSpeedOfSound + 1);
+    a.max_bounces = c.max_bounces;
+    a.sample_rate = c.sample_rate;
+    a.ir_len = r->ir_len;
+    a.delay = (int32_t)((double)c.sample_rate * 0.00044);  // devicePrograms.cu:125
+    a.is_mono = c.is_mono;
+    if (ray_end == ray_begin) return ARX_OK;
+    const int grid = trace_grid_size(ray_end - ray_begin, r->cus);
+    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    ARX_HIP(launch_trace(a, grid, r->stream));
+    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_finalize_ir(arx_renderer* r) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    const float e0 = initial_energy(r->cfg);
+    const double unit = std::ldexp((double)e0, -arx_frac_bits(n_rays(r->cfg)));
+    ARX_HIP(launch_finalize_ir((const long long*)r->hist(), r->d_ir, r->d_ir + r->ir_len, r->ir_len, unit,
+                               r->cfg.is_mono, r->stream));
+    r->conv_ir_dirty = true;
+    return ARX_OK;
+}
+
+arx_status arx_render(arx_renderer* r, double* render_ms) {
+    arx_status st = arx_clear_histogram(r);
+    if (st != ARX_OK) return st;
+    st = arx_trace_rays(r, 0, n_rays(r->cfg));
+    if (st != ARX_OK) return st;
+    st = arx_finalize_ir(r);
+    if (st != ARX_OK) return st;
+    if (render_ms) {
+        ARX_HIP(hipEventSynchronize(r->ev1));
+        float ms = 0.f;
+        ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
+        *render_ms = ms;
+    }
+    return ARX_OK;
+}
+
+arx_status arx_histogram_device(arx_renderer* r, int64_t** d_hist, size_t* n) {
+    if (!r || !d_hist) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    *d_hist = (int64_t*)r->hist();
+    if (n) *n = 2 * (size_t)r->ir_len;
+    return ARX_OK;
+}
+
+arx_status arx_attach_histogram(arx_renderer* r, int64_t* d_hist, size_t n) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (d_hist && n != 2 * (size_t)r->ir_len)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "histogram needs 2*ir_len = %zu elements, got %zu", 2 * (size_t)r->ir_len, n);
+    r->d_hist_ext = (unsigned long long*)d_hist;
+    return ARX_OK;
+}
+
+arx_status arx_ir_device(arx_renderer* r, float** d_left, float** d_right, size_t* ir_len) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (d_left) *d_left = r->d_ir;
+    if (d_right) *d_right = r->d_ir + r->ir_len;
+    if (ir_len) *ir_len = (size_t)r->ir_len;
+    return ARX_OK;
+}
+
+arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir_len) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (ir_len != (size_t)r->ir_len) return fail(ARX_ERR_INVALID_ARGUMENT, "ir_len %zu != %d", ir_len, r->ir_len);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (h_left) ARX_HIP(hipMemcpyAsync(h_left, r->d_ir, ir_len * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+    if (h_right)
+        ARX_HIP(hipMemcpyAsync(h_right, r->d_ir + r->ir_len, ir_len * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
+    if (!r || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipMemcpyAsync(r->h_counters, r->d_counters, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    r->stats.queries = r->h_counters[0];
+    r->stats.receiver_hits = r->h_counters[1];
+    r->stats.misses = r->h_counters[2];
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r->ev0, r->ev1) == hipSuccess) r->stats.trace_ms = ms;
+    *out = r->stats;
+    if (r->h_counters[3]) return fail(ARX_ERR_INTERNAL, "trace kernel reported a BVH stack overflow");
+    return ARX_OK;
+}
+
+arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right, size_t ir_len) {
+    if (!r || !h_left || !h_right) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (ir_len != (size_t)r->ir_len) return fail(ARX_ERR_INVALID_ARGUMENT, "ir_len %zu != %d", ir_len, r->ir_len);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipMemcpyAsync(r->d_ir, h_left, ir_len * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    ARX_HIP(hipMemcpyAsync(r->d_ir + r->ir_len, h_right, ir_len * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    r->conv_ir_dirty = true;
+    return ARX_OK;
+}
+
+static arx_status ensure_conv(arx_renderer* r) {
+    if (!r->conv) {
+        char err[256] = {0};
+        r->conv = conv_plan_create(r->ir_len, r->cfg.sample_rate, r->cfg.device, err, sizeof(err));
+        if (!r->conv) return fail(ARX_ERR_INTERNAL, "convolution plan: %s", err);
+        r->conv_ir_dirty = true;
+    }
+    if (r->conv_ir_dirty) {
+        ARX_HIP(conv_set_ir(r->conv, r->d_ir, r->d_ir + r->ir_len, r->stream));
+        r->conv_ir_dirty = false;
+    }
+    return ARX_OK;
+}
+
+arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
+                                float* d_out_right) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n_frames > 0 && (!d_in || !d_out_left || !d_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = ensure_conv(r);
+    if (st != ARX_OK) return st;
+    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, r->stream));
+    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t in_bytes, float* h_out_left,
+                                    float* h_out_right, double* conv_ms, double* proc_ms) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    const size_t n = in_bytes / sizeof(float);  // AudioRenderer.cpp:689: bytes / sizeof(float)
+    if (n > 0 && (!h_in || !h_out_left || !h_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    hipEvent_t p0, p1;
+    ARX_HIP(hipEventCreate(&p0));
+    ARX_HIP(hipEventCreate(&p1));
+    ARX_HIP(hipEventRecord(p0, r->stream));
+    if (n > r->conv_cap) {
+        hipFree(r->d_conv_in);
+        hipFree(r->d_conv_out);
+        r->d_conv_in = r->d_conv_out = nullptr;
+        r->conv_cap = 0;
+        ARX_HIP(hipMalloc(&r->d_conv_in, n * sizeof(float)));
+        ARX_HIP(hipMalloc(&r->d_conv_out, 2 * n * sizeof(float)));
+        r->conv_cap = n;
+    }
+    if (n > 0) ARX_HIP(hipMemcpyAsync(r->d_conv_in, h_in, n * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    arx_status st = arx_convolute_device(r, r->d_conv_in, n, r->d_conv_out, r->d_conv_out + n);
+    if (st != ARX_OK) return st;
+    if (n > 0) {
+        ARX_HIP(hipMemcpyAsync(h_out_left, r->d_conv_out, n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+        ARX_HIP(hipMemcpyAsync(h_out_right, r->d_conv_out + n, n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+    }
+    ARX_HIP(hipEventRecord(p1, r->stream));
+    ARX_HIP(hipEventSynchronize(p1));
+    float ms = 0.f;
+    if (conv_ms) {
+        ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
+        *conv_ms = ms;
+    }
+    if (proc_ms) {
+        ARX_HIP(hipEventElapsedTime(&ms, p0, p1));
+        *proc_ms = ms;
+    }
+    hipEventDestroy(p0);
+    hipEventDestroy(p1);
+    return ARX_OK;
+}
+
+arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* h_out, int device) {
+    if (count > 0 && !h_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL output");
+    if (count == 0) return ARX_OK;
+    ARX_HIP(hipSetDevice(device));
+    float* d = nullptr;
+    ARX_HIP(hipMalloc(&d, 3 * count * sizeof(float)));
+    hipError_t e = launch_ray_directions(seed, first, count, d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(h_out, d, 3 * count * sizeof(float), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(ARX_ERR_HIP, "ray directions: %s", hipGetErrorString(e));
+    return ARX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,420 @@
+// arx_conv.hip -- file-mode FFT convolution for gfx950.
+//
+// Semantics restated from R/prebuild/obj_raytracer/kernels.cu:382-438
+// (convoluteFromAudioBuffer) + AudioRenderer.cpp:706-711: the input is cut into
+// S = floor(len/sr) one-second blocks (the tail len mod sr is never processed), each
+// block is zero padded to n = ir_len and CIRCULARLY convolved (length n) with the IR,
+// the unnormalised results (n * circconv) are overlap-added at 1-s hops clipped to len,
+// and the sum is divided by (ir_len/2) (integer division).
+//
+// MI355X design: instead of 4 launches + 2 cuFFT calls + 3 device syncs per block, all
+// blocks of both channels are convolved by four batched launches:
+//   A  fwd column FFTs (length N1, in LDS) of the block PAIRS packed as re/im
+//      (x = block_2p + i*block_2p+1: one complex FFT serves two real blocks, and the
+//      inverse of (X * H) returns both results in re/im because h is real), times the
+//      four-step twiddle W_M^(n2*k1);
+//   B  per row: fwd row FFT (N2), * H_c, inverse row FFT, * W_M^(-n2*k1) -- for both
+//      channels from one forward pass (spectrum kept in registers);
+//   C  inverse column FFTs -> M * linear convolution of each block, to a f64 scratch;
+//   D  overlap-add gather with the circular fold cc[i] = lin[i] + lin[i+n], scaled
+//      n/(M*(n/2)), rounded once to f32 (deterministic, no atomics).
+// The FFT length M is the power of two >= n + sr - 1 (linear convolution, then folded
+// back to length n), so every (ir_len, sr) pair works with radix-4/2 Stockham stages.
+// All FFT arithmetic is f64: the result matches the f64 oracle to ~1e-15 relative
+// before the single f32 rounding (the "1 ULP of max|y|" bar of SURVEY.md §8c).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "arx_kernels.hpp"
+
+namespace arx {
+
+struct ConvPlan {
+    int32_t n = 0;      // ir_len (circular length of the reference)
+    int32_t sr = 0;     // hop (block length)
+    int32_t M = 0;      // FFT length (power of two)
+    int32_t N1 = 0, N2 = 0, lg1 = 0, lg2 = 0;
+    int32_t tc = 1;     // columns per workgroup in passes A / C
+    int device = 0;
+    double2* d_tw = nullptr;     // W_M^e, e in [0, M)
+    double2* d_H = nullptr;      // 2 * M, transposed layout [k1][k2]
+    double2* d_S = nullptr;      // scratch spectra: pairs_cap * 3 * M (shared + 2 channels)
+    double* d_Y = nullptr;       // per block, per channel M*lin (length n + sr - 1)
+    int64_t pairs_cap = 0;
+    char desc[160] = {0};
+};
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+// multiply by sign*i
+__device__ __forceinline__ double2 mul_si(double2 a, int sign) {
+    return sign < 0 ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
+}
+__device__ __forceinline__ double2 twiddle(const double2* __restrict__ tw, int32_t M, int64_t e, int sign) {
+    const double2 w = tw[e & (M - 1)];
+    return sign < 0 ? w : make_double2(w.x, -w.y);
+}
+
+// In-place Stockham FFT of length L = 2^lg on buf[0..L) (LDS), executed by the nt
+// threads t in [0, nt) of this group; every thread of the workgroup must call it (it
+// contains __syncthreads()).  Twiddle W_L^e = tw[e * (M/L)].
+__device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, const double2* __restrict__ tw,
+                        int32_t M) {
+    const int mstep = M >> lg;  // M / L
+    int Ns = 1;
+    int stages4 = lg >> 1;
+    for (int s = 0; s < stages4; ++s) {
+        const int quarter = L >> 2;
+        double2 v[4][4];
+        int jj[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int j = t + b * nt;
+            jj[b] = j;
+            if (j < quarter) {
+                const int k = j & (Ns - 1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double2 x = buf[j + r * quarter];
+                    if (r > 0) x = cmul(x, twiddle(tw, M, (int64_t)r * k * (L / (Ns * 4)) * mstep, sign));
+                    v[b][r] = x;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int j = jj[b];
+            if (j < quarter) {
+                const int k = j & (Ns - 1);
+                const double2 a0 = cadd(v[b][0], v[b][2]);
+                const double2 a1 = csub(v[b][0], v[b][2]);
+                const double2 a2 = cadd(v[b][1], v[b][3]);
+                const double2 a3 = mul_si(csub(v[b][1], v[b][3]), sign);
+                const int d = (j - k) * 4 + k;  // (j/Ns)*Ns*4 + j%Ns
+                buf[d] = cadd(a0, a2);
+                buf[d + Ns] = cadd(a1, a3);
+                buf[d + 2 * Ns] = csub(a0, a2);
+                buf[d + 3 * Ns] = csub(a1, a3);
+            }
+        }
+        __syncthreads();
+        Ns <<= 2;
+    }
+    if (lg & 1) {  // final radix-2 stage
+        const int half = L >> 1;
+        double2 v[8][2];
+        int jj[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int j = t + b * nt;
+            jj[b] = j;
+            if (j < half) {
+                const int k = j & (Ns - 1);
+                v[b][0] = buf[j];
+                v[b][1] = cmul(buf[j + half], twiddle(tw, M, (int64_t)k * (L / (Ns * 2)) * mstep, sign));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int j = jj[b];
+            if (j < half) {
+                const int k = j & (Ns - 1);
+                const int d = (j - k) * 2 + k;
+                buf[d] = cadd(v[b][0], v[b][1]);
+                buf[d + Ns] = csub(v[b][0], v[b][1]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct PassArgs {
+    const double2* tw;
+    int32_t M, N1, N2, lg1, lg2, tc;
+    int32_t n, sr;
+    int64_t n_blocks;   // S
+    int64_t n_pairs;
+    const float* in;    // audio input (mode 0) or IR pair base (mode 1)
+    const float* ir_l;
+    const float* ir_r;
+    double2* S;         // [pair][3][M]: 0 = forward (shared), 1/2 = per channel
+    double2* H;         // [2][M]
+    double* Y;          // [block][2][ylen]
+    int64_t ylen;       // n + sr - 1
+    float* out_l;
+    float* out_r;
+    int64_t len;
+    double scale;
+};
+
+// Pass A: forward column FFTs.  mode 0: batch = block pair p; mode 1: batch = IR channel c.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int tc = a.tc;
+    const int per = kThreads / tc;
+    const int col = threadIdx.x / per;  // local column
+    const int t = threadIdx.x % per;
+    const int64_t batch = blockIdx.y;
+    const int n2_0 = blockIdx.x * tc;
+    const int n2 = n2_0 + col;
+    double2* buf = lds + (size_t)col * a.N1;
+    // load column n2: element n1 at x[N2*n1 + n2]
+    for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
+        const int c = i % tc, n1 = i / tc;  // consecutive threads -> consecutive columns
+        const int64_t idx = (int64_t)a.N2 * n1 + n2_0 + c;
+        double2 x = make_double2(0.0, 0.0);
+        if (MODE == 0) {
+            if (idx < a.sr) {
+                const int64_t b0 = 2 * batch, b1 = 2 * batch + 1;
+                if (b0 < a.n_blocks) x.x = (double)a.in[b0 * a.sr + idx];
+                if (b1 < a.n_blocks) x.y = (double)a.in[b1 * a.sr + idx];
+            }
+        } else {
+            if (idx < a.n) x.x = (double)(batch == 0 ? a.ir_l : a.ir_r)[idx];
+        }
+        lds[(size_t)c * a.N1 + n1] = x;
+    }
+    __syncthreads();
+    lds_fft(buf, a.N1, a.lg1, -1, t, per, a.tw, a.M);
+    // twiddle W_M^(n2*k1) and store transposed: S[k1*N2 + n2]
+    double2* dst = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
+    for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
+        const int c = i % tc, k1 = i / tc;
+        const int64_t e = (int64_t)(n2_0 + c) * k1;
+        const double2 x = cmul(lds[(size_t)c * a.N1 + k1], twiddle(a.tw, a.M, e, -1));
+        dst[(int64_t)k1 * a.N2 + n2_0 + c] = x;
+    }
+}
+
+// Pass B.  mode 0: row FFT, * H_c, inverse row FFT, * W_M^(-n2*k1) for c = 0, 1.
+//          mode 1: row FFT only (IR spectrum, in place in H).
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int k1 = blockIdx.x;
+    const int64_t batch = blockIdx.y;
+    const int N2 = a.N2;
+    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
+    for (int i = threadIdx.x; i < N2; i += kThreads) lds[i] = row[i];
+    __syncthreads();
+    lds_fft(lds, N2, a.lg2, -1, threadIdx.x, kThreads, a.tw, a.M);
+    if (MODE == 1) {
+        for (int i = threadIdx.x; i < N2; i += kThreads) row[i] = lds[i];
+        return;
+    }
+    constexpr int kMaxPer = 16;  // N2 <= 4096
+    double2 keep[kMaxPer];
+#pragma unroll
+    for (int b = 0; b < kMaxPer; ++b) {
+        const int i = threadIdx.x + b * kThreads;
+        if (i < N2) keep[b] = lds[i];
+    }
+    for (int c = 0; c < 2; ++c) {
+        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * N2;
+#pragma unroll
+        for (int b = 0; b < kMaxPer; ++b) {
+            const int i = threadIdx.x + b * kThreads;
+            if (i < N2) lds[i] = cmul(keep[b], Hc[i]);
+        }
+        __syncthreads();
+        lds_fft(lds, N2, a.lg2, +1, threadIdx.x, kThreads, a.tw, a.M);
+        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
+        for (int i = threadIdx.x; i < N2; i += kThreads)
+            dst[i] = cmul(lds[i], twiddle(a.tw, a.M, (int64_t)i * k1, +1));
+        __syncthreads();
+    }
+}
+
+// Pass C: inverse column FFTs of each (pair, channel) -> M * linear convolution of the
+// two blocks of the pair (re / im), written to Y for indices < n + sr - 1.
+__global__ __launch_bounds__(kThreads) void pass_c(PassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const int tc = a.tc;
+    const int per = kThreads / tc;
+    const int col = threadIdx.x / per;
+    const int t = threadIdx.x % per;
+    const int64_t pair = blockIdx.y >> 1;
+    const int ch = blockIdx.y & 1;
+    const int n2_0 = blockIdx.x * tc;
+    const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
+    for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
+        const int c = i % tc, k1 = i / tc;
+        lds[(size_t)c * a.N1 + k1] = src[(int64_t)k1 * a.N2 + n2_0 + c];
+    }
+    __syncthreads();
+    lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, a.tw, a.M);
+    const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
+    double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
+    double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
+    for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
+        const int c = i % tc, n1 = i / tc;
+        const int64_t idx = (int64_t)a.N2 * n1 + n2_0 + c;
+        if (idx < a.ylen) {
+            const double2 v = lds[(size_t)c * a.N1 + n1];
+            if (b0 < a.n_blocks) y0[idx] = v.x;
+            if (b1 < a.n_blocks) y1[idx] = v.y;
+        }
+    }
+}
+
+// Pass D: out_c[j] = scale * sum_s (lin_s[j - s*sr] + lin_s[j - s*sr + n]) over the
+// blocks whose window [s*sr, s*sr + n) covers j (kernels.cu:425-428 clip at len).
+__global__ __launch_bounds__(kThreads) void pass_d(PassArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.len) return;
+    const int ch = blockIdx.y;
+    int64_t s_hi = j / a.sr;
+    if (s_hi > a.n_blocks - 1) s_hi = a.n_blocks - 1;
+    int64_t s_lo = (j - a.n + 1 <= 0) ? 0 : (j - a.n + 1 + a.sr - 1) / a.sr;
+    double acc = 0.0;
+    for (int64_t s = s_lo; s <= s_hi; ++s) {
+        const int64_t i = j - s * a.sr;
+        const double* y = a.Y + (s * 2 + ch) * a.ylen;
+        double v = y[i];
+        if (i + a.n < a.ylen) v += y[i + a.n];
+        acc += v;
+    }
+    (ch == 0 ? a.out_l : a.out_r)[j] = (float)(acc * a.scale);
+}
+
+int ilog2(int64_t v) {
+    int l = 0;
+    while (((int64_t)1 << l) < v) ++l;
+    return l;
+}
+
+}  // namespace
+
+ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char* err, size_t errlen) {
+    auto bad = [&](const char* m) -> ConvPlan* {
+        if (err && errlen) std::snprintf(err, errlen, "%s", m);
+        return nullptr;
+    };
+    if (ir_len <= 0 || sample_rate <= 0) return bad("ir_len and sample_rate must be positive");
+    const int64_t need = (int64_t)ir_len + (int64_t)std::min(ir_len, sample_rate) - 1;
+    const int lg = ilog2(std::max<int64_t>(need, 4));
+    if (lg > 24) return bad("FFT length above 2^24 is not supported");
+    ConvPlan* p = new ConvPlan();
+    p->n = ir_len;
+    p->sr = sample_rate;
+    p->M = 1 << lg;
+    p->lg1 = lg / 2;
+    p->lg2 = lg - p->lg1;
+    p->N1 = 1 << p->lg1;
+    p->N2 = 1 << p->lg2;
+    p->tc = std::max(1, std::min(std::min(16, p->N2), 4096 / p->N1));
+    p->device = device;
+    std::snprintf(p->desc, sizeof(p->desc), "pow2 linear+fold: n=%d sr=%d M=%d (%dx%d) f64", p->n, p->sr, p->M, p->N1,
+                  p->N2);
+    hipSetDevice(device);
+    std::vector<double2> tw((size_t)p->M);
+    const long double two_pi = 6.283185307179586476925286766559L;
+    for (int64_t e = 0; e < p->M; ++e) {
+        const long double ang = two_pi * (long double)e / (long double)p->M;
+        tw[(size_t)e] = make_double2((double)cosl(ang), -(double)sinl(ang));
+    }
+    if (hipMalloc(&p->d_tw, (size_t)p->M * sizeof(double2)) != hipSuccess ||
+        hipMalloc(&p->d_H, 2 * (size_t)p->M * sizeof(double2)) != hipSuccess ||
+        hipMemcpy(p->d_tw, tw.data(), (size_t)p->M * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess) {
+        conv_plan_destroy(p);
+        return bad("device allocation failed");
+    }
+    return p;
+}
+
+void conv_plan_destroy(ConvPlan* p) {
+    if (!p) return;
+    hipFree(p->d_tw);
+    hipFree(p->d_H);
+    hipFree(p->d_S);
+    hipFree(p->d_Y);
+    delete p;
+}
+
+const char* conv_plan_describe(const ConvPlan* p) { return p ? p->desc : ""; }
+
+static PassArgs base_args(const ConvPlan* p) {
+    PassArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.tw = p->d_tw;
+    a.M = p->M;
+    a.N1 = p->N1;
+    a.N2 = p->N2;
+    a.lg1 = p->lg1;
+    a.lg2 = p->lg2;
+    a.tc = p->tc;
+    a.n = p->n;
+    a.sr = p->sr;
+    a.H = p->d_H;
+    a.ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    return a;
+}
+
+hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
+    PassArgs a = base_args(p);
+    a.ir_l = d_ir_left;
+    a.ir_r = d_ir_right;
+    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
+    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
+    hipLaunchKernelGGL(pass_b<1>, dim3(p->N1, 2), dim3(kThreads), lds_b, s, a);
+    return hipGetLastError();
+}
+
+hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
+                    hipStream_t s) {
+    if (n_frames <= 0) return hipSuccess;
+    const int64_t S = n_frames / p->sr;  // kernels.cu:413
+    if (S == 0) {  // nothing convolved: the reference output stays zero
+        hipError_t e = hipMemsetAsync(d_out_left, 0, (size_t)n_frames * sizeof(float), s);
+        if (e == hipSuccess) e = hipMemsetAsync(d_out_right, 0, (size_t)n_frames * sizeof(float), s);
+        return e;
+    }
+    const int64_t pairs = (S + 1) / 2;
+    const int64_t ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    if (pairs > p->pairs_cap) {
+        hipFree(p->d_S);
+        hipFree(p->d_Y);
+        p->d_S = nullptr;
+        p->d_Y = nullptr;
+        p->pairs_cap = 0;
+        hipError_t e = hipMalloc(&p->d_S, (size_t)pairs * 3 * p->M * sizeof(double2));
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&p->d_Y, (size_t)pairs * 2 * 2 * ylen * sizeof(double));
+        if (e != hipSuccess) return e;
+        p->pairs_cap = pairs;
+    }
+    PassArgs a = base_args(p);
+    a.in = d_in;
+    a.S = p->d_S;
+    a.Y = p->d_Y;
+    a.n_blocks = S;
+    a.n_pairs = pairs;
+    a.len = n_frames;
+    a.out_l = d_out_left;
+    a.out_r = d_out_right;
+    a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
+    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
+    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
+    hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
+    hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
+    hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace arx

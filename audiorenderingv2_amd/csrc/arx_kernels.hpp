@@ -1,0 +1,31 @@
+// arx_kernels.hpp -- host-callable launchers for the HIP kernels (libarx.so internals).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "arx_layout.hpp"
+
+namespace arx {
+
+// Trace kernel (raygen + traversal + closest-hit + histogram, fused).
+int trace_block_size();
+int trace_grid_size(uint64_t n_rays, int device_cus);
+hipError_t launch_trace(const TraceArgs& a, int grid, hipStream_t s);
+// i64 histogram -> f32 IR (+ mono merge); unit = e0 * 2^-frac_bits.
+hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len,
+                              double unit, int32_t is_mono, hipStream_t s);
+hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
+
+// ---- convolution (arx_conv.hip) ----
+struct ConvPlan;  // opaque, defined in arx_conv.hip
+ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char* err, size_t errlen);
+void conv_plan_destroy(ConvPlan* p);
+// Spectra of the two IRs (device f32, ir_len each); must precede conv_run.
+hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s);
+// Device-resident file-mode convolution (kernels.cu:382-438 + AudioRenderer.cpp:706-711).
+hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
+                    hipStream_t s);
+const char* conv_plan_describe(const ConvPlan* p);
+
+}  // namespace arx

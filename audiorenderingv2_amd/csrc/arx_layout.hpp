@@ -1,0 +1,68 @@
+// arx_layout.hpp -- HBM data layout shared by the host builder and the HIP kernels.
+//
+// Scene (replaces the OptiX GAS + SBT, AudioRenderer.cpp:95-218, 413-464):
+//   tris  : TriRec[n_scene + n_receiver], 48 B each, in BVH leaf order so a leaf is a
+//           contiguous range (3 x 16-B loads per triangle, no index indirection).
+//           v0.w = absorption (SBT mat_absorption), v1.w = global triangle id (tie-break).
+//   nodes : BvhNode[], 64 B each (4 x 16-B loads).  Node 0 is a fixed top node whose two
+//           children are the static-scene root and the receiver root, so a listener move
+//           rewrites only the receiver sub-tree and node 0.
+// A child reference is (ref, count): count > 0 -> leaf of triangles [ref, ref+count);
+// count == 0 -> inner node index ref.  Empty children carry an inverted box.
+#pragma once
+#include <cstdint>
+
+namespace arx {
+
+struct alignas(16) TriRec {
+    float v0[3];
+    float absorption;
+    float v1[3];
+    int32_t id;
+    float v2[3];
+    int32_t pad;
+};
+static_assert(sizeof(TriRec) == 48, "TriRec must be 48 B");
+
+// Aila-Laine style node: both children's boxes side by side.
+//   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//   b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//   c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//   d = (c0.ref, c1.ref, c0.count, c1.count)
+struct alignas(16) BvhNode {
+    float a[4];
+    float b[4];
+    float c[4];
+    int32_t d[4];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+
+// LDS traversal stack depth per lane; the builder caps tree depth below it.
+constexpr int kStackDepth = 40;
+constexpr int kMaxBuildDepth = kStackDepth - 2;
+constexpr int kSpeedOfSound = 343;  // devicePrograms.cu:13
+
+// Trace kernel arguments (passed by value; lives in kernarg/SGPRs).
+struct TraceArgs {
+    const BvhNode* nodes;
+    const TriRec* tris;
+    unsigned long long* hist;       // [2*ir_len] int64 fixed point, L then R
+    unsigned long long* counters;   // [0] queries [1] receiver hits [2] misses [3] error flag
+    uint64_t seed;
+    uint64_t ray_begin;
+    uint64_t ray_end;
+    float emitter[3];
+    float center[3];
+    float e0;
+    float energy_thres;
+    float hrtf;
+    float dist_limit;
+    double inv_unit;
+    uint32_t max_bounces;
+    int32_t sample_rate;
+    int32_t ir_len;
+    int32_t delay;
+    int32_t is_mono;
+};
+
+}  // namespace arx

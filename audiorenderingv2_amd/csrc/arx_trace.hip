@@ -1,0 +1,445 @@
+// arx_trace.hip -- fused acoustic ray-trace kernel for gfx950 (MI355X).
+//
+// One lane owns one ray for its whole life (raygen -> bounce loop -> histogram),
+// replacing the OptiX pipeline of R/prebuild/obj_raytracer/devicePrograms.cu:
+//   __raygen__renderFrame   :192-254  -> trace_ray() prologue + bounce loop
+//   optixTrace / RT cores   :240-251  -> closest_hit(): software BVH2 traversal,
+//                                        per-lane LDS stack, watertight triangle test
+//   __closesthit__radiance  :62-180   -> trace_ray() hit block
+//   __miss__radiance        :186-190  -> trace_ray() miss branch
+// Work distribution: grid-stride over global ray ids.  The IR histogram is int64 fixed
+// point (unit e0*2^-frac_bits) accumulated with 64-bit atomics: order-independent,
+// bitwise reproducible and exactly summable across GPUs.
+//
+// Arithmetic is IEEE f32 with no contraction (built -ffp-contract=off) so that every
+// ray follows bit-for-bit the path computed by the CPU oracle (oracle/arx_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include "arx_kernels.hpp"
+#include "arx_layout.hpp"
+
+namespace arx {
+namespace {
+
+constexpr int kBlock = 128;
+
+// ------------------------------------------------------------------- RNG ---
+__device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                              uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0;
+        const uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f); }
+
+// cos/sin(2*pi*u), u in (0,1]: exact quadrant reduction in turns + fma Horner (same
+// coefficients and order as the oracle, so the result is bitwise identical).
+__device__ __forceinline__ void sincos_turns(double u, double& s_out, double& c_out) {
+    const double a = 4.0 * u;
+    const double q = floor(a);
+    const double f = a - q;
+    const int iq = ((int)q) & 3;
+    const double r = f * 1.5707963267948966;
+    const double r2 = r * r;
+    double ps = -1.0 / 121645100408832000.0;
+    ps = __fma_rn(ps, r2, 1.0 / 355687428096000.0);
+    ps = __fma_rn(ps, r2, -1.0 / 1307674368000.0);
+    ps = __fma_rn(ps, r2, 1.0 / 6227020800.0);
+    ps = __fma_rn(ps, r2, -1.0 / 39916800.0);
+    ps = __fma_rn(ps, r2, 1.0 / 362880.0);
+    ps = __fma_rn(ps, r2, -1.0 / 5040.0);
+    ps = __fma_rn(ps, r2, 1.0 / 120.0);
+    ps = __fma_rn(ps, r2, -1.0 / 6.0);
+    const double sr = __fma_rn(r * r2, ps, r);
+    double pc = 1.0 / 2432902008176640000.0;
+    pc = __fma_rn(pc, r2, -1.0 / 6402373705728000.0);
+    pc = __fma_rn(pc, r2, 1.0 / 20922789888000.0);
+    pc = __fma_rn(pc, r2, -1.0 / 87178291200.0);
+    pc = __fma_rn(pc, r2, 1.0 / 479001600.0);
+    pc = __fma_rn(pc, r2, -1.0 / 3628800.0);
+    pc = __fma_rn(pc, r2, 1.0 / 40320.0);
+    pc = __fma_rn(pc, r2, -1.0 / 720.0);
+    pc = __fma_rn(pc, r2, 1.0 / 24.0);
+    pc = __fma_rn(pc, r2, -1.0 / 2.0);
+    const double cr = __fma_rn(r2, pc, 1.0);
+    double c, s;
+    if (iq == 0) {
+        c = cr;
+        s = sr;
+    } else if (iq == 1) {
+        c = -sr;
+        s = cr;
+    } else if (iq == 2) {
+        c = -cr;
+        s = -sr;
+    } else {
+        c = sr;
+        s = -cr;
+    }
+    s_out = s;
+    c_out = c;
+}
+
+// devicePrograms.cu:216-224 with Philox(seed, ray id) instead of curand(clock64(), tid).
+__device__ __forceinline__ float3 ray_direction(uint64_t seed, uint64_t rid) {
+    uint32_t c0 = (uint32_t)rid, c1 = (uint32_t)(rid >> 32), c2 = 0u, c3 = 0u;
+    philox4x32_10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float u1 = u01(c0);
+    const float u2 = u01(c1);
+    const double cz = 2.0 * (double)u2 - 1.0;
+    const double sz = __dsqrt_rn(1.0 - cz * cz);
+    double st, ct;
+    sincos_turns((double)u1, st, ct);
+    return make_float3((float)(sz * ct), (float)(sz * st), (float)cz);
+}
+
+// ------------------------------------------------------------ geometry ---
+struct Ray {
+    float o[3];      // origin
+    float op[3];     // origin permuted (kx, ky, kz)
+    float inv[3];    // safe reciprocal direction (box test only)
+    float sx, sy, sz;
+    int kx, ky, kz;
+};
+
+__device__ __forceinline__ float sel3(float x, float y, float z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
+
+__device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
+    r.o[0] = o.x;
+    r.o[1] = o.y;
+    r.o[2] = o.z;
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const int kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
+    int kx = kz + 1;
+    if (kx == 3) kx = 0;
+    int ky = kx + 1;
+    if (ky == 3) ky = 0;
+    const float dkz = sel3(d.x, d.y, d.z, kz);
+    if (dkz < 0.0f) {
+        const int t = kx;
+        kx = ky;
+        ky = t;
+    }
+    r.kx = kx;
+    r.ky = ky;
+    r.kz = kz;
+    r.sx = sel3(d.x, d.y, d.z, kx) / dkz;
+    r.sy = sel3(d.x, d.y, d.z, ky) / dkz;
+    r.sz = 1.0f / dkz;
+    r.op[0] = sel3(o.x, o.y, o.z, kx);
+    r.op[1] = sel3(o.x, o.y, o.z, ky);
+    r.op[2] = sel3(o.x, o.y, o.z, kz);
+    const float dd[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float v = dd[k];
+        if (fabsf(v) < 1e-20f) v = (v < 0.0f) ? -1e-20f : 1e-20f;
+        r.inv[k] = 1.0f / v;
+    }
+}
+
+// Watertight ray/triangle test (Woop, Benthin, Wald 2013); t >= 0 (optixTrace tmin 0).
+// Vertex components are selected by (kx,ky,kz) then differenced against the permuted
+// origin: the same values as A[k] = v[k] - o[k] indexed afterwards (oracle order).
+struct Hit {
+    float U, V, W, det, t;
+};
+
+__device__ __forceinline__ bool tri_test(const Ray& r, float4 p0, float4 p1, float4 p2, Hit& h) {
+    const float Ax = sel3(p0.x, p0.y, p0.z, r.kx) - r.op[0];
+    const float Ay = sel3(p0.x, p0.y, p0.z, r.ky) - r.op[1];
+    const float Az = sel3(p0.x, p0.y, p0.z, r.kz) - r.op[2];
+    const float Bx = sel3(p1.x, p1.y, p1.z, r.kx) - r.op[0];
+    const float By = sel3(p1.x, p1.y, p1.z, r.ky) - r.op[1];
+    const float Bz = sel3(p1.x, p1.y, p1.z, r.kz) - r.op[2];
+    const float Cx = sel3(p2.x, p2.y, p2.z, r.kx) - r.op[0];
+    const float Cy = sel3(p2.x, p2.y, p2.z, r.ky) - r.op[1];
+    const float Cz = sel3(p2.x, p2.y, p2.z, r.kz) - r.op[2];
+    const float ax = Ax - r.sx * Az;
+    const float ay = Ay - r.sy * Az;
+    const float bx = Bx - r.sx * Bz;
+    const float by = By - r.sy * Bz;
+    const float cx = Cx - r.sx * Cz;
+    const float cy = Cy - r.sy * Cz;
+    const float U = cx * by - cy * bx;
+    const float V = ax * cy - ay * cx;
+    const float W = bx * ay - by * ax;
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    const float det = U + V + W;
+    if (det == 0.0f) return false;
+    const float az = r.sz * Az;
+    const float bz = r.sz * Bz;
+    const float cz = r.sz * Cz;
+    const float T = U * az + V * bz + W * cz;
+    const float t = T / det;
+    if (!(t >= 0.0f)) return false;
+    h.U = U;
+    h.V = V;
+    h.W = W;
+    h.det = det;
+    h.t = t;
+    return true;
+}
+
+__device__ __forceinline__ void leaf_hits(const TriRec* __restrict__ tris, const Ray& r, int first, int count,
+                                          float& best_t, int& best_id, int& best) {
+    for (int k = 0; k < count; ++k) {
+        const float4* tp = reinterpret_cast<const float4*>(tris + first + k);
+        const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
+        Hit h;
+        if (tri_test(r, p0, p1, p2, h)) {
+            const int id = __float_as_int(p1.w);
+            if (h.t < best_t || (h.t == best_t && id < best_id)) {
+                best_t = h.t;
+                best_id = id;
+                best = first + k;
+            }
+        }
+    }
+}
+
+// Closest hit over the two-level BVH (node 0 = top).  Returns the TriRec index or -1.
+__device__ __forceinline__ int closest_hit(const TraceArgs& a, const Ray& r, int* __restrict__ stk, int lane,
+                                           bool& overflow) {
+    float best_t = __builtin_huge_valf();
+    int best_id = 0x7fffffff;
+    int best = -1;
+    int sp = 0;
+    int node = 0;
+    const float ox = r.o[0], oy = r.o[1], oz = r.o[2];
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    while (true) {
+        const float4* np = reinterpret_cast<const float4*>(a.nodes + node);
+        const float4 na = np[0];
+        const float4 nb = np[1];
+        const float4 nc = np[2];
+        const int4 nd = *reinterpret_cast<const int4*>(np + 3);
+        // child 0
+        const float x00 = (na.x - ox) * ix, x01 = (na.y - ox) * ix;
+        const float y00 = (na.z - oy) * iy, y01 = (na.w - oy) * iy;
+        const float z00 = (nc.x - oz) * iz, z01 = (nc.y - oz) * iz;
+        const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+        const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), best_t));
+        // child 1
+        const float x10 = (nb.x - ox) * ix, x11 = (nb.y - ox) * ix;
+        const float y10 = (nb.z - oy) * iy, y11 = (nb.w - oy) * iy;
+        const float z10 = (nc.z - oz) * iz, z11 = (nc.w - oz) * iz;
+        const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+        const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), best_t));
+        bool h0 = tn0 <= tf0;
+        bool h1 = tn1 <= tf1;
+        if (h0 && nd.z > 0) {
+            leaf_hits(a.tris, r, nd.x, nd.z, best_t, best_id, best);
+            h0 = false;
+        }
+        if (h1 && nd.w > 0) {
+            leaf_hits(a.tris, r, nd.y, nd.w, best_t, best_id, best);
+            h1 = false;
+        }
+        if (h0 && h1) {
+            const bool swap = tn1 < tn0;
+            const int near_n = swap ? nd.y : nd.x;
+            const int far_n = swap ? nd.x : nd.y;
+            if (sp < kStackDepth) {
+                stk[sp * kBlock + lane] = far_n;
+                ++sp;
+            } else {
+                overflow = true;
+            }
+            node = near_n;
+        } else if (h0) {
+            node = nd.x;
+        } else if (h1) {
+            node = nd.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stk[sp * kBlock + lane];
+        }
+    }
+    return best;
+}
+
+// glm-style helpers (glm::dot is x*x + y*y + z*z left to right)
+__device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float3 sub3(float3 a, float3 b) { return make_float3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ float3 add3(float3 a, float3 b) { return make_float3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ float3 scale3(float s, float3 a) { return make_float3(s * a.x, s * a.y, s * a.z); }
+
+__device__ __forceinline__ void hist_add(unsigned long long* h, int k, float e, double inv_unit) {
+    const long long q = __double2ll_rn((double)e * inv_unit);
+    if (q != 0) atomicAdd(h + k, (unsigned long long)q);
+}
+
+__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs a) {
+    __shared__ int stk[kStackDepth * kBlock];
+    const int lane = threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    bool overflow = false;
+    const float3 center = make_float3(a.center[0], a.center[1], a.center[2]);
+    unsigned long long* const hl = a.hist;
+    unsigned long long* const hr = a.hist + a.ir_len;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + lane; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        float3 dir = ray_direction(a.seed, a.ray_begin + i);
+        float3 pos = make_float3(a.emitter[0], a.emitter[1], a.emitter[2]);
+        float e = a.e0;
+        float dist = 0.0f;
+        int depth = 0;
+        if (!(dir.x != 0.0f || dir.y != 0.0f || dir.z != 0.0f)) continue;  // :230
+        while (dist < a.dist_limit && e > a.energy_thres && depth >= 0 && (uint32_t)depth < a.max_bounces) {
+            ++n_q;
+            Ray r;
+            setup_ray(r, pos, dir);
+            const int hit = closest_hit(a, r, stk, lane, overflow);
+            if (hit < 0) {  // __miss__radiance
+                ++n_miss;
+                depth = -1;
+                break;
+            }
+            const float4* tp = reinterpret_cast<const float4*>(a.tris + hit);
+            const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
+            const float3 P1 = make_float3(p0.x, p0.y, p0.z);
+            const float3 P2 = make_float3(p1.x, p1.y, p1.z);
+            const float3 P3 = make_float3(p2.x, p2.y, p2.z);
+            const float ab = p0.w;
+            // Ng = normalize(cross(P2-P1, P3-P1))  (:75-77)
+            const float3 U = sub3(P2, P1), V = sub3(P3, P1);
+            const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
+            const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
+            Hit h;
+            tri_test(r, p0, p1, p2, h);
+            const float bu = h.V / h.det;
+            const float bv = h.W / h.det;
+            const float w0 = (1.0f - bu) - bv;
+            const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
+            const float3 seg = sub3(P, pos);
+            dist += sqrtf(dot3(seg, seg));  // :83
+            if (ab < 0.0f) {                // receiver chord weighting, r = 1 (:91-122)
+                const float3 nd = scale3(1.0f / sqrtf(dot3(dir, dir)), dir);
+                const float3 oc = sub3(P, center);
+                const float qa = dot3(nd, nd);
+                const float qb = 2.0f * dot3(oc, nd);
+                const float qc = dot3(oc, oc) - 1.0f;
+                const float disc = qb * qb - (4.0f * qa) * qc;
+                if (disc <= 0.0f) {
+                    e = 0.0f;
+                } else {
+                    const float sq = sqrtf(disc);
+                    const float t1 = (-qb - sq) / (2.0f * qa);
+                    const float t2 = (-qb + sq) / (2.0f * qa);
+                    const float3 i1 = add3(P, scale3(t1, nd));
+                    const float3 i2 = add3(P, scale3(t2, nd));
+                    const float3 di = sub3(i1, i2);
+                    e = e * sqrtf(dot3(di, di));
+                }
+            }
+            if (ab == -1.0f || ab == -2.0f) {  // receiver halves (:128-170)
+                ++n_rx;
+                const int k = (int)roundf((dist / (float)kSpeedOfSound) * (float)a.sample_rate);
+                if (k < a.ir_len) {
+                    unsigned long long* own = (ab == -1.0f) ? hl : hr;
+                    unsigned long long* other = (ab == -1.0f) ? hr : hl;
+                    hist_add(own, k, e, a.inv_unit);
+                    if (!a.is_mono) {
+                        const int kk = (k + a.delay < a.ir_len) ? k + a.delay : k;
+                        hist_add(other, kk, e * (1.0f - a.hrtf), a.inv_unit);
+                    }
+                }
+                depth = -1;
+            } else {  // specular reflection + absorption (:173-175)
+                const float s2 = 2.0f * dot3(dir, Ng);
+                dir = sub3(dir, scale3(s2, Ng));
+                e = e * (1.0f - ab);
+                ++depth;
+            }
+            pos = add3(P, scale3(1e-3f, dir));  // :179
+        }
+    }
+    // wave-reduce the counters, one atomic per wave
+    unsigned int vq = n_q, vr = n_rx, vm = n_miss, vo = overflow ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        vq += __shfl_xor(vq, off, 64);
+        vr += __shfl_xor(vr, off, 64);
+        vm += __shfl_xor(vm, off, 64);
+        vo |= __shfl_xor(vo, off, 64);
+    }
+    if ((lane & 63) == 0) {
+        if (vq) atomicAdd(a.counters + 0, (unsigned long long)vq);
+        if (vr) atomicAdd(a.counters + 1, (unsigned long long)vr);
+        if (vm) atomicAdd(a.counters + 2, (unsigned long long)vm);
+        if (vo) atomicOr(a.counters + 3, 1ull);
+    }
+}
+
+__global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __restrict__ L, float* __restrict__ R,
+                                   int32_t ir_len, double unit, int32_t mono) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ir_len) return;
+    float l = (float)((double)hist[k] * unit);
+    float r = (float)((double)hist[ir_len + k] * unit);
+    if (mono) {  // addIRs (kernels.cu:519-527)
+        const float s = l + r;
+        l = s;
+        r = s;
+    }
+    L[k] = l;
+    R[k] = r;
+}
+
+__global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, float* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float3 d = ray_direction(seed, first + i);
+    out[3 * i + 0] = d.x;
+    out[3 * i + 1] = d.y;
+    out[3 * i + 2] = d.z;
+}
+
+}  // namespace
+
+int trace_block_size() { return kBlock; }
+
+int trace_grid_size(uint64_t n_rays, int device_cus) {
+    const uint64_t blocks = (n_rays + kBlock - 1) / kBlock;
+    const uint64_t cap = (uint64_t)(device_cus > 0 ? device_cus : 256) * 16;
+    return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+}
+
+hipError_t launch_trace(const TraceArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(trace_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len, double unit,
+                              int32_t is_mono, hipStream_t s) {
+    const int b = 256;
+    const int g = (ir_len + b - 1) / b;
+    if (g > 0) hipLaunchKernelGGL(finalize_ir_kernel, dim3(g), dim3(b), 0, s, hist, ir_left, ir_right, ir_len, unit, is_mono);
+    return hipGetLastError();
+}
+
+hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s) {
+    const int b = 256;
+    const uint64_t g = (count + b - 1) / b;
+    if (g > 0) hipLaunchKernelGGL(ray_dir_kernel, dim3((unsigned)g), dim3(b), 0, s, seed, first, count, d_out);
+    return hipGetLastError();
+}
+
+}  // namespace arx

@@ -1,0 +1,200 @@
+"""Python host mirror of the reference's AudioRenderer (R/prebuild/obj_raytracer/AudioRenderer.h:16-152).
+
+Method names follow the reference so callers and tests read like the original:
+render(), convoluteAudioFile(), setEmitterPosInOptix(), setSphereCenterInOptix(),
+setThresholds(), set_hrtf_absorption_rate(), setBasePower(), setMonoOutput().  Every
+call goes through libarx.so's C ABI (include/arx.h); there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import ArxConfig, ArxStats, check, fptr, lib
+from .scene import Scene
+
+
+@dataclass
+class RenderSettings:
+    rays: tuple = (100, 100, 100)          # pathtracer_parameters.rays (Context.cpp:125-133)
+    ir_length_in_seconds: int = 2          # renderer_parameters.ir_length_in_seconds
+    sample_rate: int = 44100               # audio file rate (Context.cpp:197-224)
+    base_power: float = 100.0
+    energy_thres: float = 0.0
+    max_bounces: int = 10
+    hrtf_absorption_rate: float = 1.0      # round(0.9), Context.cpp:145
+    mono: bool = False
+    seed: int = 1
+    device: int = 0
+
+    def to_c(self) -> ArxConfig:
+        c = ArxConfig()
+        c.rays_x, c.rays_y, c.rays_z = (int(v) for v in self.rays)
+        c.ir_length_in_seconds = int(self.ir_length_in_seconds)
+        c.sample_rate = int(self.sample_rate)
+        c.base_power = float(self.base_power)
+        c.energy_thres = float(self.energy_thres)
+        c.max_bounces = int(self.max_bounces)
+        c.hrtf_absorption_rate = float(self.hrtf_absorption_rate)
+        c.is_mono = 1 if self.mono else 0
+        c.seed = int(self.seed)
+        c.device = int(self.device)
+        return c
+
+
+class AudioRenderer:
+    """AudioRenderer(model, ir_length_in_seconds, sample_rate, materials, rays) (AudioRenderer.h:24)."""
+
+    def __init__(self, settings: RenderSettings, scene: Scene | None = None,
+                 receiver: tuple[np.ndarray, np.ndarray] | None = None):
+        self.settings = settings
+        self._h = C.c_void_p()
+        cfg = settings.to_c()
+        check(lib().arx_create(C.byref(cfg), C.byref(self._h)))
+        self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
+        if receiver is not None:
+            self.set_receiver_model(*receiver)
+        if scene is not None:
+            self.set_scene(scene)
+
+    # -- lifecycle ---------------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            lib().arx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -- scene -------------------------------------------------------------------
+    def set_scene(self, scene: Scene) -> None:
+        self._scene_v = np.ascontiguousarray(scene.tri_v, np.float32)
+        self._scene_a = np.ascontiguousarray(scene.tri_abs, np.float32)
+        check(lib().arx_set_scene(self._h, fptr(self._scene_v), fptr(self._scene_a), scene.n_tris))
+
+    def set_receiver_model(self, left: np.ndarray, right: np.ndarray) -> None:
+        for side, t in enumerate((left, right)):
+            t = np.ascontiguousarray(t, np.float32).reshape(-1, 9)
+            check(lib().arx_set_receiver_model(self._h, side, fptr(t), t.shape[0]))
+
+    def setEmitterPosInOptix(self, pos) -> None:  # AudioRenderer.cpp:752-756
+        check(lib().arx_set_emitter(self._h, *(float(v) for v in pos)))
+
+    def setSphereCenterInOptix(self, pos, yaw_deg: float = 0.0) -> None:
+        """placeReceiver(...) + setSphereCenterInOptix (AudioRenderer.cpp:758-762)."""
+        check(lib().arx_set_listener(self._h, *(float(v) for v in pos), float(yaw_deg)))
+
+    place_listener = setSphereCenterInOptix
+
+    def setThresholds(self, energy: float, max_bounces: int) -> None:
+        check(lib().arx_set_thresholds(self._h, float(energy), int(max_bounces)))
+
+    def set_hrtf_absorption_rate(self, rate: float) -> None:
+        check(lib().arx_set_hrtf_absorption_rate(self._h, float(rate)))
+
+    def setBasePower(self, p: float) -> None:
+        check(lib().arx_set_base_power(self._h, float(p)))
+
+    def setMonoOutput(self, mono: bool) -> None:
+        check(lib().arx_set_mono_output(self._h, 1 if mono else 0))
+
+    def set_seed(self, seed: int) -> None:
+        check(lib().arx_set_seed(self._h, int(seed)))
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        check(lib().arx_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    # -- render ------------------------------------------------------------------
+    def render(self) -> float:
+        """AudioRenderer::render (AudioRenderer.cpp:489-523); returns the trace kernel's ms."""
+        ms = C.c_double()
+        check(lib().arx_render(self._h, C.byref(ms)))
+        return ms.value
+
+    def clear_histogram(self) -> None:
+        check(lib().arx_clear_histogram(self._h))
+
+    def trace_rays(self, ray_begin: int, ray_end: int) -> None:
+        check(lib().arx_trace_rays(self._h, int(ray_begin), int(ray_end)))
+
+    def finalize_ir(self) -> None:
+        check(lib().arx_finalize_ir(self._h))
+
+    def histogram_device_ptr(self) -> tuple[int, int]:
+        p = C.c_void_p()
+        n = C.c_size_t()
+        check(lib().arx_histogram_device(self._h, C.byref(p), C.byref(n)))
+        return int(p.value), int(n.value)
+
+    def attach_histogram(self, d_ptr: int | None, n_elems: int = 0) -> None:
+        check(lib().arx_attach_histogram(self._h, C.c_void_p(d_ptr or 0), int(n_elems)))
+
+    def ir_device_ptrs(self) -> tuple[int, int, int]:
+        l, r, n = C.c_void_p(), C.c_void_p(), C.c_size_t()
+        check(lib().arx_ir_device(self._h, C.byref(l), C.byref(r), C.byref(n)))
+        return int(l.value), int(r.value), int(n.value)
+
+    def get_ir(self) -> tuple[np.ndarray, np.ndarray]:
+        L = np.empty(self.ir_length, np.float32)
+        R = np.empty(self.ir_length, np.float32)
+        check(lib().arx_copy_ir(self._h, fptr(L), fptr(R), self.ir_length))
+        return L, R
+
+    def set_ir(self, left: np.ndarray, right: np.ndarray) -> None:
+        L = np.ascontiguousarray(left, np.float32)
+        R = np.ascontiguousarray(right, np.float32)
+        check(lib().arx_set_ir(self._h, fptr(L), fptr(R), L.size))
+
+    def stats(self) -> dict:
+        s = ArxStats()
+        check(lib().arx_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in ArxStats._fields_}
+
+    # -- convolution ---------------------------------------------------------------
+    def convoluteAudioFile(self, samples: np.ndarray) -> tuple[np.ndarray, np.ndarray, float, float]:
+        """AudioRenderer::convoluteAudioFile (AudioRenderer.cpp:663-750): host in, host out."""
+        x = np.ascontiguousarray(samples, np.float32)
+        L = np.zeros_like(x)
+        R = np.zeros_like(x)
+        cms, pms = C.c_double(), C.c_double()
+        check(lib().arx_convolute_audio_file(self._h, fptr(x), x.nbytes, fptr(L), fptr(R), C.byref(cms),
+                                             C.byref(pms)))
+        return L, R, cms.value, pms.value
+
+    def convolute_device(self, d_in: int, n_frames: int, d_out_left: int, d_out_right: int) -> None:
+        check(lib().arx_convolute_device(self._h, C.c_void_p(d_in), n_frames, C.c_void_p(d_out_left),
+                                         C.c_void_p(d_out_right)))
+
+
+def place_receiver_vertices(local_xyz: np.ndarray, pos, yaw_deg: float) -> np.ndarray:
+    """place_receiver_half's transform (OptixModel.cpp:178-193), host-only."""
+    v = np.ascontiguousarray(local_xyz, np.float32).reshape(-1, 3)
+    out = np.empty_like(v)
+    check(lib().arx_place_receiver_vertices(fptr(v), v.shape[0], *(float(p) for p in pos), float(yaw_deg),
+                                            fptr(out)))
+    return out
+
+
+def debug_ray_directions(seed: int, first: int, count: int, device: int = 0) -> np.ndarray:
+    out = np.empty((count, 3), np.float32)
+    check(lib().arx_debug_ray_directions(seed, first, count, fptr(out), device))
+    return out
+
+
+def frac_bits(n_rays: int) -> int:
+    return int(lib().arx_frac_bits(n_rays))

@@ -1,0 +1,156 @@
+/*
+ * arx.h -- C ABI of the MI355X acoustic impulse-response engine (libarx.so).
+ *
+ * Drop-in boundary for the GPU path of sgrazi/AudioRenderingV2's obj_raytracer.
+ * The reference exposes that path as the C++ class AudioRenderer
+ * (R/prebuild/obj_raytracer/AudioRenderer.h:16-152) over free CUDA/cuFFT
+ * functions (R/prebuild/obj_raytracer/kernels.cuh:17-28).  Every entry point
+ * below names the reference member/function it replaces.  Plain pointers and
+ * sizes only; no C++ or torch types.  Every call returns an arx_status
+ * (the reference throws or exit()s: optix7.h:8-45, kernels.cu:7-68); the
+ * message of the last failure on the calling thread is arx_last_error().
+ *
+ * Threading: one renderer is driven by one host thread at a time (the
+ * reference's AudioRenderer is not thread-safe either, AudioRenderer.h; the
+ * app serialises it with output_buffer_mutex, main.cpp:38-63).  All GPU work
+ * is issued on the renderer's HIP stream (arx_set_stream), never the null
+ * stream; calls that return host data synchronise that stream.
+ */
+#ifndef ARX_H
+#define ARX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARX_ABI_VERSION 1
+
+typedef enum arx_status {
+    ARX_OK = 0,
+    ARX_ERR_INVALID_ARGUMENT = 1,
+    ARX_ERR_HIP = 2,          /* HIP runtime / kernel failure (reference: CUDA_CHECK throw) */
+    ARX_ERR_OUT_OF_MEMORY = 3,
+    ARX_ERR_NOT_READY = 4,    /* e.g. render before a scene was set */
+    ARX_ERR_IO = 5,
+    ARX_ERR_INTERNAL = 6      /* device-side invariant violated (e.g. BVH stack overflow) */
+} arx_status;
+
+typedef struct arx_renderer arx_renderer;
+
+/* Construction parameters: Context::loadContext (R/prebuild/obj_raytracer/Context.cpp:15-236)
+ * feeding AudioRenderer(model, ir_length_in_seconds, sample_rate, materials, rays)
+ * (AudioRenderer.h:24) and the setters called before render (main.cpp:548-553). */
+typedef struct arx_config {
+    int32_t rays_x, rays_y, rays_z;     /* rays.{x,y,z}; N = x*y*z (Context.cpp:125-133) */
+    uint32_t ir_length_in_seconds;      /* renderer_parameters.ir_length_in_seconds (rounded) */
+    int32_t sample_rate;                /* audio file rate, 44100 in live mode (Context.cpp:197-224) */
+    float base_power;                   /* pathtracer_parameters.base_power */
+    float energy_thres;                 /* ray_energy_threshold */
+    uint32_t max_bounces;               /* ray_max_bounces (rounded) */
+    float hrtf_absorption_rate;         /* round()ed by the reference config reader (Context.cpp:145) */
+    int32_t is_mono;                    /* scene_parameters.mono */
+    uint64_t seed;                      /* Philox key; replaces curand_init(clock64(), tid) (devicePrograms.cu:216-217) */
+    int32_t device;                     /* HIP device ordinal (reference hard-codes 0, AudioRenderer.cpp:252) */
+} arx_config;
+
+typedef struct arx_stats {
+    uint64_t queries;        /* closest-hit queries issued (== optixTrace calls) */
+    uint64_t receiver_hits;  /* rays terminated on a receiver half */
+    uint64_t misses;         /* rays terminated by __miss__radiance */
+    double trace_ms;         /* device time of the last trace kernel (HIP events) */
+    double conv_ms;          /* device time of the last convolution */
+    int64_t n_scene_tris, n_receiver_tris, n_nodes;
+    int32_t bvh_depth;
+} arx_stats;
+
+const char* arx_status_string(arx_status s);
+const char* arx_last_error(void);
+int arx_abi_version(void);
+void arx_default_config(arx_config* cfg); /* the reference's defaults (Context.cpp:19-117) */
+
+/* AudioRenderer::AudioRenderer (AudioRenderer.h:24; AudioRenderer.cpp:60-93):
+ * allocates the IR histogram/IR buffers (ir_len = ir_length_in_seconds*sample_rate bins). */
+arx_status arx_create(const arx_config* cfg, arx_renderer** out);
+void arx_destroy(arx_renderer* r);
+arx_status arx_get_config(const arx_renderer* r, arx_config* out);
+/* Issue all work on this hipStream_t (NULL -> the renderer's own stream). */
+arx_status arx_set_stream(arx_renderer* r, void* hip_stream);
+void* arx_get_stream(const arx_renderer* r);
+
+/* Static scene geometry: AudioRenderer::buildAccel + buildSBT (AudioRenderer.cpp:95-218, 413-464),
+ * with getMaterialAbsorption (:34-56) already applied per triangle by the caller
+ * (arx_material_absorption).  tri_vertices: n_tris*9 floats (P1,P2,P3 in mesh index order);
+ * triangle order is the global id used to break equal-distance ties.  Builds the
+ * SAH BVH on the host and uploads it (once; receivers are kept in a separate sub-tree). */
+arx_status arx_set_scene(arx_renderer* r, const float* tri_vertices, const float* tri_absorption,
+                         int64_t n_tris);
+/* The two receiver half-spheres in their local frame: HalfSphere (HalfSphere.cpp:3-31) loaded
+ * from leftHalf.obj (side 0) / rightHalf.obj (side 1); n_tris*9 floats. */
+arx_status arx_set_receiver_model(arx_renderer* r, int side, const float* tri_vertices_local,
+                                  int64_t n_tris);
+/* place_receiver_half's vertex transform alone (OptixModel.cpp:178-193): v' = (x,y,z) +
+ * rotate(-radians(yaw), +Y) * v with glm's operation order; host-only, no device needed. */
+arx_status arx_place_receiver_vertices(const float* local_xyz, int64_t n_vertices, float x, float y, float z,
+                                       float yaw_deg, float* out_xyz);
+/* getMaterialAbsorption (AudioRenderer.cpp:34-56): receiver_left -1, receiver_right -2,
+ * exact name match in the config list, else 0.5. */
+float arx_material_absorption(const char* name, const char* const* names, const float* absorption,
+                              size_t n_materials);
+
+/* setEmitterPosInOptix (AudioRenderer.cpp:752-756). */
+arx_status arx_set_emitter(arx_renderer* r, float x, float y, float z);
+/* placeReceiver + setSphereCenterInOptix (OptixModel.cpp:153-257, AudioRenderer.cpp:758-762):
+ * receiver halves rotated by -yaw about +Y, translated to (x,y,z); sphere center = (x,y,z).
+ * Rebuilds only the receiver sub-tree (no full rebuild, unlike reload() :466-486). */
+arx_status arx_set_listener(arx_renderer* r, float x, float y, float z, float yaw_deg);
+arx_status arx_set_thresholds(arx_renderer* r, float energy, uint32_t max_bounces); /* :764-768 */
+arx_status arx_set_hrtf_absorption_rate(arx_renderer* r, float rate);             /* :770-773 */
+arx_status arx_set_base_power(arx_renderer* r, float base_power);                 /* :775-778 */
+arx_status arx_set_mono_output(arx_renderer* r, int mono);                        /* :800-803 */
+arx_status arx_set_seed(arx_renderer* r, uint64_t seed);
+
+/* AudioRenderer::render (AudioRenderer.h:27; AudioRenderer.cpp:489-523): clear, trace all
+ * N rays, finalize the stereo IR (mono merge = addIRs, kernels.cu:519-527).  render_ms gets the
+ * trace kernel's device time (the reference's timed window, :495-518). */
+arx_status arx_render(arx_renderer* r, double* render_ms);
+
+/* Building blocks of render() for ray-sharded multi-GPU use (no reference equivalent; the
+ * reference is single-GPU).  The histogram is 2*ir_len int64 in device memory: [L | R],
+ * fixed point with unit e0*2^-frac_bits, so a sum over shards (RCCL int64 SUM) is exact. */
+arx_status arx_clear_histogram(arx_renderer* r);
+arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end); /* global ray ids */
+arx_status arx_histogram_device(arx_renderer* r, int64_t** d_hist, size_t* n_elems);
+/* Accumulate into caller-owned device memory (2*ir_len int64, e.g. a torch tensor that RCCL
+ * all-reduces in place); NULL restores the renderer's own buffer. */
+arx_status arx_attach_histogram(arx_renderer* r, int64_t* d_hist, size_t n_elems);
+arx_status arx_finalize_ir(arx_renderer* r);
+arx_status arx_ir_device(arx_renderer* r, float** d_left, float** d_right, size_t* ir_len);
+arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir_len);
+arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
+/* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
+ * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
+ * from render()). */
+arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right, size_t ir_len);
+int arx_frac_bits(uint64_t n_rays_total);
+
+/* AudioRenderer::convoluteAudioFile (AudioRenderer.h:31; AudioRenderer.cpp:663-750) over
+ * convoluteFromAudioBuffer (kernels.cuh:21; kernels.cu:382-438): 1-s blocks zero padded to
+ * ir_len, circular convolution with each IR, overlap-added, tail (len mod sr) unprocessed,
+ * divided by (ir_len/2).  Host buffers, sizes in BYTES like the reference. */
+arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t in_bytes, float* h_out_left,
+                                    float* h_out_right, double* convolute_ms, double* process_ms);
+/* Same on device-resident buffers (n_frames floats each); no host synchronisation. */
+arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
+                                float* d_out_right);
+
+/* Debug / parity hooks. */
+arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
+                                    int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARX_H */

@@ -1,0 +1,43 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def world_scene(scene, listener, yaw=0.0):
+    """Static scene + placed receiver halves, in the global-id order the engine uses
+    (scene, receiver_left, receiver_right: placeReceiver, OptixModel.cpp:153-157)."""
+    from audiorenderingv2_amd import place_receiver_vertices, receiver_local
+
+    L, R = receiver_local()
+    Lw = place_receiver_vertices(L.reshape(-1, 3), listener, yaw).reshape(-1, 9)
+    Rw = place_receiver_vertices(R.reshape(-1, 3), listener, yaw).reshape(-1, 9)
+    tv = np.concatenate([scene.tri_v, Lw, Rw]).astype(np.float32)
+    ta = np.concatenate([scene.tri_abs, np.full(len(Lw), -1.0, np.float32),
+                         np.full(len(Rw), -2.0, np.float32)]).astype(np.float32)
+    return tv, ta
+
+
+@pytest.fixture(scope="session")
+def c1_scene():
+    from audiorenderingv2_amd.scene import reference_config_materials, test_obj_scene
+
+    return test_obj_scene(reference_config_materials())
+
+
+@pytest.fixture(scope="session")
+def conference():
+    from audiorenderingv2_amd.scene import conference_standin
+
+    return conference_standin()

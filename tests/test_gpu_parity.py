@@ -1,0 +1,235 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (DESIGN.md "Parity"):
+  * ray directions, per-ray paths and the i64 IR histogram: BIT-EXACT (integer work);
+    the f32 IR is a deterministic function of the histogram, so it is bit-exact too;
+  * convolution: max |gpu - oracle_f32| <= 1 ULP(max |oracle|) (the north star's
+    "within 1 ULP", as a norm-wise bound);
+  * full BASELINE sizes: size-independent properties (determinism, shard-sum
+    exactness, inverse-square energy, linearity of the convolution).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from audiorenderingv2_amd import AudioRenderer, RenderSettings, debug_ray_directions, receiver_local
+from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, Scene
+from conftest import world_scene
+
+pytestmark = pytest.mark.gpu
+
+
+def make(scene, listener, yaw=0.0, emitter=(0.0, 0.0, 0.0), **kw):
+    s = RenderSettings(**kw)
+    r = AudioRenderer(s, scene=scene, receiver=receiver_local())
+    r.setEmitterPosInOptix(emitter)
+    r.setSphereCenterInOptix(listener, yaw)
+    return r
+
+
+def oracle_run(scene, listener, yaw, emitter, s: RenderSettings, threads=8, bvh=True):
+    tv, ta = world_scene(scene, listener, yaw)
+    osc = po.Scene(tv, ta, bvh=bvh)
+    p = po.make_params(rays=s.rays, sample_rate=s.sample_rate, ir_seconds=s.ir_length_in_seconds,
+                       base_power=s.base_power, energy_thres=s.energy_thres, max_bounces=s.max_bounces,
+                       hrtf=s.hrtf_absorption_rate, mono=s.mono, seed=s.seed, emitter=emitter, listener=listener)
+    L, R, st = osc.trace(p, threads=threads)
+    irl, irr = po.finalize_ir(p, L, R)
+    return irl, irr, st
+
+
+def assert_same_render(r, scene, listener, yaw, emitter, s):
+    r.render()
+    gl, gr = r.get_ir()
+    st = r.stats()
+    ol, orr, ost = oracle_run(scene, listener, yaw, emitter, s)
+    assert (st["queries"], st["receiver_hits"], st["misses"]) == (ost["queries"], ost["receiver_hits"], ost["misses"])
+    assert np.array_equal(gl.view(np.uint32), ol.view(np.uint32))
+    assert np.array_equal(gr.view(np.uint32), orr.view(np.uint32))
+    return gl, gr, st
+
+
+def test_ray_directions_bitwise():
+    for first in (0, (1 << 32) - 50000):
+        g = debug_ray_directions(5, first, 100000)
+        o = po.ray_directions(5, first, 100000)
+        assert np.array_equal(g.view(np.uint32), o.view(np.uint32)), first
+
+
+def test_c1_reference_config(c1_scene):
+    """BASELINE configs[0]: test.obj, 1024 rays x 2 bounces, 16 kHz, R/config.json placement."""
+    s = RenderSettings(rays=(32, 32, 1), sample_rate=16000, base_power=3.62, max_bounces=2)
+    r = make(c1_scene, (2.5, 9.9, 0.0), **s.__dict__)
+    assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, (0.0, 0.0, 0.0), s)
+
+
+def test_c1_dense_bitwise(c1_scene):
+    s = RenderSettings(rays=(64, 64, 8), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
+    r = make(c1_scene, (2.5, 9.9, 0.0), **s.__dict__)
+    gl, gr, st = assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, (0.0, 0.0, 0.0), s)
+    assert st["receiver_hits"] > 0 and gl.any() and gr.any()
+
+
+def test_conference_bitwise(conference):
+    s = RenderSettings(rays=(40, 40, 10), sample_rate=16000, base_power=3.62, max_bounces=8)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    gl, gr, st = assert_same_render(r, conference, CONFERENCE_LISTENER, 0.0, CONFERENCE_EMITTER, s)
+    assert st["receiver_hits"] > 0
+
+
+def test_conference_48k_rotated_mono_bitwise(conference):
+    s = RenderSettings(rays=(30, 40, 10), sample_rate=48000, base_power=3.62, max_bounces=16, mono=True,
+                       hrtf_absorption_rate=0.25, seed=99)
+    lst, yaw = (3.0, 1.5, -1.0), 75.0
+    r = make(conference, lst, yaw=yaw, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    gl, gr, _ = assert_same_render(r, conference, lst, yaw, CONFERENCE_EMITTER, s)
+    assert np.array_equal(gl, gr)
+
+
+def test_listener_move_equals_fresh_renderer(conference):
+    s = RenderSettings(rays=(20, 20, 10), sample_rate=16000, base_power=3.62, max_bounces=8)
+    r = make(conference, (0.0, 1.0, 0.0), emitter=CONFERENCE_EMITTER, **s.__dict__)
+    r.render()
+    r.setSphereCenterInOptix((4.0, 1.3, -2.0), 200.0)  # no scene rebuild: receiver sub-tree only
+    r.render()
+    a = r.get_ir()
+    f = make(conference, (4.0, 1.3, -2.0), yaw=200.0, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    f.render()
+    b = f.get_ir()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_shards_sum_exactly(conference):
+    s = RenderSettings(rays=(100, 100, 10), sample_rate=48000, base_power=3.62, max_bounces=16)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    r.render()
+    full = r.get_ir()
+    q_full = r.stats()["queries"]
+    r.clear_histogram()
+    n = 100 * 100 * 10
+    for b, e in ((0, 12345), (12345, 60000), (60000, n)):
+        r.trace_rays(b, e)
+    r.finalize_ir()
+    parts = r.get_ir()
+    assert r.stats()["queries"] == q_full
+    assert np.array_equal(full[0], parts[0]) and np.array_equal(full[1], parts[1])
+
+
+def test_full_size_c3_properties(conference):
+    """configs[2] size: 1M rays x 16 bounces, 48 kHz -- determinism + shard exactness."""
+    s = RenderSettings(rays=(100, 100, 100), sample_rate=48000, base_power=3.62, max_bounces=16)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    r.render()
+    a = r.get_ir()
+    st = r.stats()
+    r.render()
+    b = r.get_ir()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert st["queries"] <= 16 * 10**6 and st["queries"] > 10 * 10**6
+    assert st["receiver_hits"] > 1000
+    # an independent 4-way shard (as 4 GPUs would run it) gives the identical histogram
+    r.clear_histogram()
+    for k in range(4):
+        r.trace_rays(k * 250000, (k + 1) * 250000)
+    r.finalize_ir()
+    c = r.get_ir()
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1])
+    # and it matches the oracle on a ray sample of the same launch (ray ids 0..3999)
+    r.clear_histogram()
+    r.trace_rays(0, 4000)
+    tv, ta = world_scene(conference, CONFERENCE_LISTENER, 0.0)
+    osc = po.Scene(tv, ta, bvh=True)
+    p = po.make_params(rays=s.rays, sample_rate=48000, base_power=3.62, max_bounces=16,
+                       emitter=CONFERENCE_EMITTER, listener=CONFERENCE_LISTENER)
+    L, R, ost = osc.trace(p, 0, 4000, threads=8)
+    h_ptr, n = r.histogram_device_ptr()
+    assert r.stats()["queries"] == ost["queries"]
+    r.finalize_ir()
+    ol, orr = po.finalize_ir(p, L, R)
+    gl, gr = r.get_ir()
+    assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
+
+
+def test_inverse_square_on_gpu():
+    d = 4.0
+    empty = Scene(np.zeros((0, 9), np.float32), np.zeros(0, np.float32), [])
+    s = RenderSettings(rays=(1000, 1000, 1), sample_rate=16000, base_power=3.62, max_bounces=4)
+    r = make(empty, (d, 0.0, 0.0), **s.__dict__)
+    r.render()
+    gl, gr = r.get_ir()
+    total = gl.astype(np.float64).sum() + gr.astype(np.float64).sum()
+    integral = 2 * math.pi * (1 - (d * d - 1) / (2 * d) * math.log((d + 1) / (d - 1)))
+    expect = float(np.float32(3.62)) / (4 * math.pi * 4.18879020478) * integral
+    assert abs(total / expect - 1) < 0.02
+
+
+# ------------------------------------------------------------------ convolution ---
+def ulp_of_max(y):
+    return np.spacing(np.float32(np.abs(y).max()))
+
+
+def conv_renderer(sr, secs=2):
+    return AudioRenderer(RenderSettings(rays=(1, 1, 1), sample_rate=sr, ir_length_in_seconds=secs))
+
+
+def sparse_ir(n, rng, k=300, scale=1e-4):
+    ir = np.zeros(n, np.float32)
+    ir[rng.integers(0, n, k)] = rng.exponential(scale, k).astype(np.float32)
+    return ir
+
+
+@pytest.mark.parametrize("sr,secs,length", [(1000, 2, 10555), (1000, 2, 999), (1000, 2, 4000), (800, 3, 7777),
+                                            (16000, 2, 128000), (441, 2, 5000)])
+def test_convolution_matches_oracle(sr, secs, length):
+    rng = np.random.default_rng(sr + length)
+    n = sr * secs
+    irl, irr = sparse_ir(n, rng), sparse_ir(n, rng)
+    x = (0.3 * rng.standard_normal(length)).astype(np.float32)
+    r = conv_renderer(sr, secs)
+    r.set_ir(irl, irr)
+    L, R, _, _ = r.convoluteAudioFile(x)
+    for got, ir in ((L, irl), (R, irr)):
+        ref = po.convolute_audio(x, sr, ir)
+        if not ref.any():
+            assert not got.any()
+        else:
+            assert np.abs(got - ref).max() <= ulp_of_max(ref)
+
+
+def test_convolution_c3_size_with_rendered_ir(conference):
+    """configs[2] audio shape: 807498 frames @ 48 kHz (A_Clapper_Board length), IR from a render."""
+    s = RenderSettings(rays=(100, 100, 20), sample_rate=48000, base_power=3.62, max_bounces=16)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    r.render()
+    irl, irr = r.get_ir()
+    rng = np.random.default_rng(0)
+    t = np.arange(807498) / 48000.0
+    x = (0.5 * np.sin(2 * np.pi * 440 * t) * np.exp(-t % 1.0 * 3) + 0.05 * rng.standard_normal(t.size)).astype(np.float32)
+    L, R, _, _ = r.convoluteAudioFile(x)
+    for got, ir in ((L, irl), (R, irr)):
+        ref = po.convolute_audio(x, 48000, ir)
+        assert np.abs(got - ref).max() <= ulp_of_max(ref)
+    # linearity (size-independent property): conv(2x) == 2 conv(x) up to rounding
+    L2, _, _, _ = r.convoluteAudioFile(2 * x)
+    assert np.abs(L2 - 2 * L).max() <= 2 * ulp_of_max(2 * L)
+
+
+def test_convolution_device_api_equals_host_api():
+    torch = pytest.importorskip("torch")
+    sr = 16000
+    rng = np.random.default_rng(3)
+    r = conv_renderer(sr)
+    irl, irr = sparse_ir(2 * sr, rng), sparse_ir(2 * sr, rng)
+    r.set_ir(irl, irr)
+    x = rng.standard_normal(5 * sr + 17).astype(np.float32)
+    L, R, _, _ = r.convoluteAudioFile(x)
+    dx = torch.from_numpy(x).cuda()
+    dl = torch.empty_like(dx)
+    dr = torch.empty_like(dx)
+    torch.cuda.synchronize()
+    r.convolute_device(dx.data_ptr(), x.size, dl.data_ptr(), dr.data_ptr())
+    import audiorenderingv2_amd._lib as L_
+    L_.check(L_.lib().arx_copy_ir(r.handle, None, None, r.ir_length))  # syncs the renderer stream
+    assert np.array_equal(dl.cpu().numpy(), L) and np.array_equal(dr.cpu().numpy(), R)
