@@ -169,7 +169,7 @@ ChildRef empty_child() {
         c.hi[k] = -1e30f;
     }
     c.ref = 0;
-    c.count = 0;  // never traversed: the inverted box rejects every ray
+    c.count = -1;  // empty: the kernel skips count < 0 (a min/max slab test would accept an inverted box)
     return c;
 }
 
@@ -217,12 +217,35 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 }
 
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset) {
-    auto fix = [&](int32_t& ref, int32_t count) { ref += (count > 0) ? tri_offset : node_offset; };
+    auto fix = [&](int32_t& ref, int32_t count) {
+        if (count >= 0) ref += (count > 0) ? tri_offset : node_offset;
+    };
     for (BvhNode& n : b.nodes) {
         fix(n.d[0], n.d[2]);
         fix(n.d[1], n.d[3]);
     }
-    if (!(b.root.count == 0 && b.root.lo[0] > b.root.hi[0])) fix(b.root.ref, b.root.count);
+    fix(b.root.ref, b.root.count);
+}
+
+bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why) {
+    // Every inner child must have a larger index than its parent (the builder emits nodes in
+    // pre-order): that makes the graph acyclic, so traversal always terminates.
+    for (size_t i = 0; i < n_nodes; ++i) {
+        for (int c = 0; c < 2; ++c) {
+            const int32_t ref = nodes[i].d[c], count = nodes[i].d[2 + c];
+            if (count < 0) continue;
+            if (count > 0) {
+                if (ref < 0 || (size_t)ref + (size_t)count > n_tris) {
+                    *why = "leaf range out of bounds";
+                    return false;
+                }
+            } else if (ref <= (int64_t)i || (size_t)ref >= n_nodes) {
+                *why = "inner child index not after its parent";
+                return false;
+            }
+        }
+    }
+    return true;
 }
 
 }  // namespace arx

@@ -29,5 +29,7 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
 BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
 ChildRef empty_child();
+// Structural check of a device-ready node array (acyclic, references in range).
+bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why);
 
 }  // namespace arx

@@ -183,6 +183,16 @@ arx_status ensure_device_scene(arx_renderer* r) {
     }
     if (full || r->recv_dirty) {
         BvhNode top = make_node(r->scene.root, r->recv.root);
+        {
+            std::vector<BvhNode> all;
+            all.reserve(n_nodes);
+            all.push_back(top);
+            all.insert(all.end(), r->scene.nodes.begin(), r->scene.nodes.end());
+            all.insert(all.end(), r->recv.nodes.begin(), r->recv.nodes.end());
+            const char* why = "";
+            if (!validate_bvh(all.data(), all.size(), n_tris, &why))
+                return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
+        }
         ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         if (full && !r->scene.nodes.empty())
             ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(), r->scene.nodes.size() * sizeof(BvhNode),
@@ -326,7 +336,7 @@ arx_status arx_get_config(const arx_renderer* r, arx_config* out) {
 
 arx_status arx_set_stream(arx_renderer* r, void* s) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
-    r->stream = s ? (hipStream_t)s : r->own_stream;
+    r->stream = (hipStream_t)s;
     return ARX_OK;
 }
 
@@ -452,6 +462,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.ir_len = r->ir_len;
     a.delay = (int32_t)((double)c.sample_rate * 0.00044);  // devicePrograms.cu:125
     a.is_mono = c.is_mono;
+    a.max_visits = (int32_t)std::min<size_t>(r->nodes_cap + 8, 0x7fffffff);
     if (ray_end == ray_begin) return ARX_OK;
     const int grid = trace_grid_size(ray_end - ray_begin, r->cus);
     ARX_HIP(hipEventRecord(r->ev0, r->stream));

@@ -63,6 +63,7 @@ struct TraceArgs {
     int32_t ir_len;
     int32_t delay;
     int32_t is_mono;
+    int32_t max_visits;  // traversal guard: > number of inner nodes (each is visited at most once)
 };
 
 }  // namespace arx

@@ -223,7 +223,12 @@ __device__ __forceinline__ int closest_hit(const TraceArgs& a, const Ray& r, int
     int node = 0;
     const float ox = r.o[0], oy = r.o[1], oz = r.o[2];
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    int visits = 0;
     while (true) {
+        if (++visits > a.max_visits) {  // malformed tree guard: never spin forever
+            overflow = true;
+            break;
+        }
         const float4* np = reinterpret_cast<const float4*>(a.nodes + node);
         const float4 na = np[0];
         const float4 nb = np[1];
@@ -241,8 +246,8 @@ __device__ __forceinline__ int closest_hit(const TraceArgs& a, const Ray& r, int
         const float z10 = (nc.z - oz) * iz, z11 = (nc.w - oz) * iz;
         const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
         const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), best_t));
-        bool h0 = tn0 <= tf0;
-        bool h1 = tn1 <= tf1;
+        bool h0 = tn0 <= tf0 && nd.z >= 0;  // count < 0: empty child
+        bool h1 = tn1 <= tf1 && nd.w >= 0;
         if (h0 && nd.z > 0) {
             leaf_hits(a.tris, r, nd.x, nd.z, best_t, best_id, best);
             h0 = false;

@@ -117,7 +117,11 @@ class AudioRenderer:
         check(lib().arx_set_seed(self._h, int(seed)))
 
     def set_stream(self, stream_ptr: int | None) -> None:
+        """Issue work on this hipStream_t (e.g. torch.cuda.Stream().cuda_stream); 0/None = null stream."""
         check(lib().arx_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def get_stream(self) -> int:
+        return int(lib().arx_get_stream(self._h) or 0)
 
     # -- render ------------------------------------------------------------------
     def render(self) -> float:

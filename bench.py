@@ -152,7 +152,10 @@ def main(argv=None) -> int:
     r = AudioRenderer(settings, scene=scene, receiver=receiver)
     r.setEmitterPosInOptix(CONFERENCE_EMITTER)
     r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-    stream = torch.cuda.current_stream(dev)
+    # one dedicated (non-null) stream for the renderer AND torch/RCCL, so the trace kernel,
+    # the all-reduce, the convolution and the timing events are ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     ir_len = r.ir_length
     hist = torch.zeros(2 * ir_len, dtype=torch.int64, device=dev)

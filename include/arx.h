@@ -76,7 +76,8 @@ void arx_default_config(arx_config* cfg); /* the reference's defaults (Context.c
 arx_status arx_create(const arx_config* cfg, arx_renderer** out);
 void arx_destroy(arx_renderer* r);
 arx_status arx_get_config(const arx_renderer* r, arx_config* out);
-/* Issue all work on this hipStream_t (NULL -> the renderer's own stream). */
+/* Issue all work on this hipStream_t, used as given (NULL = the legacy null stream).  The
+ * renderer starts on a non-blocking stream of its own; arx_get_stream returns the current one. */
 arx_status arx_set_stream(arx_renderer* r, void* hip_stream);
 void* arx_get_stream(const arx_renderer* r);
 
