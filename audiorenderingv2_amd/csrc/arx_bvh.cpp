@@ -239,6 +239,10 @@ bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const cha
                     *why = "leaf range out of bounds";
                     return false;
                 }
+                if (count > 15 || ref >= (1 << 27)) {  // stack leaf tag: -(first*16 + count) - 1
+                    *why = "leaf larger than 15 triangles or beyond 2^27 (degenerate scene)";
+                    return false;
+                }
             } else if (ref <= (int64_t)i || (size_t)ref >= n_nodes) {
                 *why = "inner child index not after its parent";
                 return false;

@@ -463,10 +463,10 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.delay = (int32_t)((double)c.sample_rate * 0.00044);  // devicePrograms.cu:125
     a.is_mono = c.is_mono;
     a.max_visits = (int32_t)std::min<size_t>(r->nodes_cap + 8, 0x7fffffff);
+    a.bvh_depth = r->stats.bvh_depth;
     if (ray_end == ray_begin) return ARX_OK;
-    const int grid = trace_grid_size(ray_end - ray_begin, r->cus);
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
-    ARX_HIP(launch_trace(a, grid, r->stream));
+    ARX_HIP(launch_trace(a, r->cus, r->stream));
     ARX_HIP(hipEventRecord(r->ev1, r->stream));
     return ARX_OK;
 }

@@ -11,7 +11,9 @@ namespace arx {
 // Trace kernel (raygen + traversal + closest-hit + histogram, fused).
 int trace_block_size();
 int trace_grid_size(uint64_t n_rays, int device_cus);
-hipError_t launch_trace(const TraceArgs& a, int grid, hipStream_t s);
+// cus = compute units of the device (grid sizing); the variant comes from ARX_TRACE_KERNEL.
+hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s);
+int trace_variant();
 // i64 histogram -> f32 IR (+ mono merge); unit = e0 * 2^-frac_bits.
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len,
                               double unit, int32_t is_mono, hipStream_t s);

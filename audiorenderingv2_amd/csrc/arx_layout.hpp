@@ -38,8 +38,9 @@ struct alignas(16) BvhNode {
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
 // LDS traversal stack depth per lane; the builder caps tree depth below it.
-constexpr int kStackDepth = 40;
-constexpr int kMaxBuildDepth = kStackDepth - 2;
+constexpr int kStackDepth = 40;      // v1/v2 (A/B variants): trees up to depth 39
+constexpr int kMaxStackDepth = 64;   // deepest stack variant of the default kernel
+constexpr int kMaxBuildDepth = kMaxStackDepth - 2;
 constexpr int kSpeedOfSound = 343;  // devicePrograms.cu:13
 
 // Trace kernel arguments (passed by value; lives in kernarg/SGPRs).
@@ -64,6 +65,7 @@ struct TraceArgs {
     int32_t delay;
     int32_t is_mono;
     int32_t max_visits;  // traversal guard: > number of inner nodes (each is visited at most once)
+    int32_t bvh_depth;   // inner levels on the longest root path (top node included) = max stack use
 };
 
 }  // namespace arx

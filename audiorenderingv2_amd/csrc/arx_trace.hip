@@ -15,6 +15,8 @@
 // ray follows bit-for-bit the path computed by the CPU oracle (oracle/arx_oracle.c).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
 
@@ -213,71 +215,84 @@ __device__ __forceinline__ void leaf_hits(const TriRec* __restrict__ tris, const
     }
 }
 
-// Closest hit over the two-level BVH (node 0 = top).  Returns the TriRec index or -1.
-__device__ __forceinline__ int closest_hit(const TraceArgs& a, const Ray& r, int* __restrict__ stk, int lane,
-                                           bool& overflow) {
-    float best_t = __builtin_huge_valf();
-    int best_id = 0x7fffffff;
-    int best = -1;
-    int sp = 0;
-    int node = 0;
+// Per-lane traversal state of one closest-hit query over the two-level BVH (node 0 = top).
+struct Trav {
+    float best_t;
+    int best_id;
+    int best;    // TriRec index of the closest hit so far, -1 = none
+    int node;    // inner node to visit next
+    int sp;      // LDS stack depth
+    int visits;
+};
+
+__device__ __forceinline__ void trav_init(Trav& t) {
+    t.best_t = __builtin_huge_valf();
+    t.best_id = 0x7fffffff;
+    t.best = -1;
+    t.node = 0;
+    t.sp = 0;
+    t.visits = 0;
+}
+
+// One traversal step: visit t.node (test both children, intersect leaf children in place,
+// descend near-first / pop).  Returns false when the query is finished.
+template <int BLOCK, int STACK>
+__device__ __forceinline__ bool trav_step(const TraceArgs& a, const Ray& r, Trav& t, int* __restrict__ stk, int lane,
+                                          bool& overflow) {
+    if (++t.visits > a.max_visits) {  // malformed tree guard: never spin forever
+        overflow = true;
+        return false;
+    }
+    const float4* np = reinterpret_cast<const float4*>(a.nodes + t.node);
+    const float4 na = np[0];
+    const float4 nb = np[1];
+    const float4 nc = np[2];
+    const int4 nd = *reinterpret_cast<const int4*>(np + 3);
     const float ox = r.o[0], oy = r.o[1], oz = r.o[2];
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
-    int visits = 0;
-    while (true) {
-        if (++visits > a.max_visits) {  // malformed tree guard: never spin forever
-            overflow = true;
-            break;
-        }
-        const float4* np = reinterpret_cast<const float4*>(a.nodes + node);
-        const float4 na = np[0];
-        const float4 nb = np[1];
-        const float4 nc = np[2];
-        const int4 nd = *reinterpret_cast<const int4*>(np + 3);
-        // child 0
-        const float x00 = (na.x - ox) * ix, x01 = (na.y - ox) * ix;
-        const float y00 = (na.z - oy) * iy, y01 = (na.w - oy) * iy;
-        const float z00 = (nc.x - oz) * iz, z01 = (nc.y - oz) * iz;
-        const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
-        const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), best_t));
-        // child 1
-        const float x10 = (nb.x - ox) * ix, x11 = (nb.y - ox) * ix;
-        const float y10 = (nb.z - oy) * iy, y11 = (nb.w - oy) * iy;
-        const float z10 = (nc.z - oz) * iz, z11 = (nc.w - oz) * iz;
-        const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
-        const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), best_t));
-        bool h0 = tn0 <= tf0 && nd.z >= 0;  // count < 0: empty child
-        bool h1 = tn1 <= tf1 && nd.w >= 0;
-        if (h0 && nd.z > 0) {
-            leaf_hits(a.tris, r, nd.x, nd.z, best_t, best_id, best);
-            h0 = false;
-        }
-        if (h1 && nd.w > 0) {
-            leaf_hits(a.tris, r, nd.y, nd.w, best_t, best_id, best);
-            h1 = false;
-        }
-        if (h0 && h1) {
-            const bool swap = tn1 < tn0;
-            const int near_n = swap ? nd.y : nd.x;
-            const int far_n = swap ? nd.x : nd.y;
-            if (sp < kStackDepth) {
-                stk[sp * kBlock + lane] = far_n;
-                ++sp;
-            } else {
-                overflow = true;
-            }
-            node = near_n;
-        } else if (h0) {
-            node = nd.x;
-        } else if (h1) {
-            node = nd.y;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = stk[sp * kBlock + lane];
-        }
+    // child 0
+    const float x00 = (na.x - ox) * ix, x01 = (na.y - ox) * ix;
+    const float y00 = (na.z - oy) * iy, y01 = (na.w - oy) * iy;
+    const float z00 = (nc.x - oz) * iz, z01 = (nc.y - oz) * iz;
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    // child 1
+    const float x10 = (nb.x - ox) * ix, x11 = (nb.y - ox) * ix;
+    const float y10 = (nb.z - oy) * iy, y11 = (nb.w - oy) * iy;
+    const float z10 = (nc.z - oz) * iz, z11 = (nc.w - oz) * iz;
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    bool h0 = tn0 <= tf0 && nd.z >= 0;  // count < 0: empty child
+    bool h1 = tn1 <= tf1 && nd.w >= 0;
+    if (h0 && nd.z > 0) {
+        leaf_hits(a.tris, r, nd.x, nd.z, t.best_t, t.best_id, t.best);
+        h0 = false;
     }
-    return best;
+    if (h1 && nd.w > 0) {
+        leaf_hits(a.tris, r, nd.y, nd.w, t.best_t, t.best_id, t.best);
+        h1 = false;
+    }
+    if (h0 && h1) {
+        const bool swap = tn1 < tn0;
+        const int near_n = swap ? nd.y : nd.x;
+        const int far_n = swap ? nd.x : nd.y;
+        if (t.sp < STACK) {
+            stk[t.sp * BLOCK + lane] = far_n;
+            ++t.sp;
+        } else {
+            overflow = true;
+        }
+        t.node = near_n;
+    } else if (h0) {
+        t.node = nd.x;
+    } else if (h1) {
+        t.node = nd.y;
+    } else {
+        if (t.sp == 0) return false;
+        --t.sp;
+        t.node = stk[t.sp * BLOCK + lane];
+    }
+    return true;
 }
 
 // glm-style helpers (glm::dot is x*x + y*y + z*z left to right)
@@ -291,92 +306,102 @@ __device__ __forceinline__ void hist_add(unsigned long long* h, int k, float e, 
     if (q != 0) atomicAdd(h + k, (unsigned long long)q);
 }
 
-__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs a) {
-    __shared__ int stk[kStackDepth * kBlock];
-    const int lane = threadIdx.x;
-    const uint64_t n = a.ray_end - a.ray_begin;
-    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
-    bool overflow = false;
-    const float3 center = make_float3(a.center[0], a.center[1], a.center[2]);
-    unsigned long long* const hl = a.hist;
-    unsigned long long* const hr = a.hist + a.ir_len;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + lane; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        float3 dir = ray_direction(a.seed, a.ray_begin + i);
-        float3 pos = make_float3(a.emitter[0], a.emitter[1], a.emitter[2]);
-        float e = a.e0;
-        float dist = 0.0f;
-        int depth = 0;
-        if (!(dir.x != 0.0f || dir.y != 0.0f || dir.z != 0.0f)) continue;  // :230
-        while (dist < a.dist_limit && e > a.energy_thres && depth >= 0 && (uint32_t)depth < a.max_bounces) {
-            ++n_q;
-            Ray r;
-            setup_ray(r, pos, dir);
-            const int hit = closest_hit(a, r, stk, lane, overflow);
-            if (hit < 0) {  // __miss__radiance
-                ++n_miss;
-                depth = -1;
-                break;
-            }
-            const float4* tp = reinterpret_cast<const float4*>(a.tris + hit);
-            const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
-            const float3 P1 = make_float3(p0.x, p0.y, p0.z);
-            const float3 P2 = make_float3(p1.x, p1.y, p1.z);
-            const float3 P3 = make_float3(p2.x, p2.y, p2.z);
-            const float ab = p0.w;
-            // Ng = normalize(cross(P2-P1, P3-P1))  (:75-77)
-            const float3 U = sub3(P2, P1), V = sub3(P3, P1);
-            const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
-            const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
-            Hit h;
-            tri_test(r, p0, p1, p2, h);
-            const float bu = h.V / h.det;
-            const float bv = h.W / h.det;
-            const float w0 = (1.0f - bu) - bv;
-            const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
-            const float3 seg = sub3(P, pos);
-            dist += sqrtf(dot3(seg, seg));  // :83
-            if (ab < 0.0f) {                // receiver chord weighting, r = 1 (:91-122)
-                const float3 nd = scale3(1.0f / sqrtf(dot3(dir, dir)), dir);
-                const float3 oc = sub3(P, center);
-                const float qa = dot3(nd, nd);
-                const float qb = 2.0f * dot3(oc, nd);
-                const float qc = dot3(oc, oc) - 1.0f;
-                const float disc = qb * qb - (4.0f * qa) * qc;
-                if (disc <= 0.0f) {
-                    e = 0.0f;
-                } else {
-                    const float sq = sqrtf(disc);
-                    const float t1 = (-qb - sq) / (2.0f * qa);
-                    const float t2 = (-qb + sq) / (2.0f * qa);
-                    const float3 i1 = add3(P, scale3(t1, nd));
-                    const float3 i2 = add3(P, scale3(t2, nd));
-                    const float3 di = sub3(i1, i2);
-                    e = e * sqrtf(dot3(di, di));
-                }
-            }
-            if (ab == -1.0f || ab == -2.0f) {  // receiver halves (:128-170)
-                ++n_rx;
-                const int k = (int)roundf((dist / (float)kSpeedOfSound) * (float)a.sample_rate);
-                if (k < a.ir_len) {
-                    unsigned long long* own = (ab == -1.0f) ? hl : hr;
-                    unsigned long long* other = (ab == -1.0f) ? hr : hl;
-                    hist_add(own, k, e, a.inv_unit);
-                    if (!a.is_mono) {
-                        const int kk = (k + a.delay < a.ir_len) ? k + a.delay : k;
-                        hist_add(other, kk, e * (1.0f - a.hrtf), a.inv_unit);
-                    }
-                }
-                depth = -1;
-            } else {  // specular reflection + absorption (:173-175)
-                const float s2 = 2.0f * dot3(dir, Ng);
-                dir = sub3(dir, scale3(s2, Ng));
-                e = e * (1.0f - ab);
-                ++depth;
-            }
-            pos = add3(P, scale3(1e-3f, dir));  // :179
+// Per-lane ray state (PRD, PRD.h:5-14, minus the pointer plumbing).
+struct RayState {
+    float3 pos, dir;
+    float e, dist;
+    int depth;
+};
+
+// Loop guard of __raygen__renderFrame (devicePrograms.cu:233-236).
+__device__ __forceinline__ bool wants_query(const TraceArgs& a, const RayState& s) {
+    return s.dist < a.dist_limit && s.e > a.energy_thres && s.depth >= 0 && (uint32_t)s.depth < a.max_bounces;
+}
+
+__device__ __forceinline__ void ray_init(const TraceArgs& a, RayState& s, uint64_t rid) {
+    s.dir = ray_direction(a.seed, rid);
+    s.pos = make_float3(a.emitter[0], a.emitter[1], a.emitter[2]);
+    s.e = a.e0;
+    s.dist = 0.0f;
+    s.depth = 0;
+    if (!(s.dir.x != 0.0f || s.dir.y != 0.0f || s.dir.z != 0.0f)) s.depth = -1;  // :230, no trace
+}
+
+// __closesthit__radiance (devicePrograms.cu:62-180) for TriRec `hit`, or __miss__radiance
+// (:186-190) when hit < 0.  r is the ray the query was traced with.
+__device__ __forceinline__ void shade(const TraceArgs& a, RayState& s, const Ray& r, int hit, uint32_t& n_rx,
+                                      uint32_t& n_miss) {
+    if (hit < 0) {
+        ++n_miss;
+        s.depth = -1;
+        return;
+    }
+    const float4* tp = reinterpret_cast<const float4*>(a.tris + hit);
+    const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
+    const float3 P1 = make_float3(p0.x, p0.y, p0.z);
+    const float3 P2 = make_float3(p1.x, p1.y, p1.z);
+    const float3 P3 = make_float3(p2.x, p2.y, p2.z);
+    const float ab = p0.w;
+    // Ng = normalize(cross(P2-P1, P3-P1))  (:75-77)
+    const float3 U = sub3(P2, P1), V = sub3(P3, P1);
+    const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
+    const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
+    Hit h;
+    tri_test(r, p0, p1, p2, h);
+    const float bu = h.V / h.det;
+    const float bv = h.W / h.det;
+    const float w0 = (1.0f - bu) - bv;
+    const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
+    const float3 seg = sub3(P, s.pos);
+    s.dist += sqrtf(dot3(seg, seg));  // :83
+    float e = s.e;
+    if (ab < 0.0f) {  // receiver chord weighting, r = 1 (:91-122)
+        const float3 center = make_float3(a.center[0], a.center[1], a.center[2]);
+        const float3 nd = scale3(1.0f / sqrtf(dot3(s.dir, s.dir)), s.dir);
+        const float3 oc = sub3(P, center);
+        const float qa = dot3(nd, nd);
+        const float qb = 2.0f * dot3(oc, nd);
+        const float qc = dot3(oc, oc) - 1.0f;
+        const float disc = qb * qb - (4.0f * qa) * qc;
+        if (disc <= 0.0f) {
+            e = 0.0f;
+        } else {
+            const float sq = sqrtf(disc);
+            const float t1 = (-qb - sq) / (2.0f * qa);
+            const float t2 = (-qb + sq) / (2.0f * qa);
+            const float3 i1 = add3(P, scale3(t1, nd));
+            const float3 i2 = add3(P, scale3(t2, nd));
+            const float3 di = sub3(i1, i2);
+            e = e * sqrtf(dot3(di, di));
         }
     }
-    // wave-reduce the counters, one atomic per wave
+    if (ab == -1.0f || ab == -2.0f) {  // receiver halves (:128-170)
+        ++n_rx;
+        const int k = (int)roundf((s.dist / (float)kSpeedOfSound) * (float)a.sample_rate);
+        if (k < a.ir_len) {
+            unsigned long long* hl = a.hist;
+            unsigned long long* hr = a.hist + a.ir_len;
+            unsigned long long* own = (ab == -1.0f) ? hl : hr;
+            unsigned long long* other = (ab == -1.0f) ? hr : hl;
+            hist_add(own, k, e, a.inv_unit);
+            if (!a.is_mono) {
+                const int kk = (k + a.delay < a.ir_len) ? k + a.delay : k;
+                hist_add(other, kk, e * (1.0f - a.hrtf), a.inv_unit);
+            }
+        }
+        s.depth = -1;
+    } else {  // specular reflection + absorption (:173-175)
+        const float s2 = 2.0f * dot3(s.dir, Ng);
+        s.dir = sub3(s.dir, scale3(s2, Ng));
+        e = e * (1.0f - ab);
+        ++s.depth;
+    }
+    s.e = e;
+    s.pos = add3(P, scale3(1e-3f, s.dir));  // :179
+}
+
+__device__ __forceinline__ void flush_counters(const TraceArgs& a, uint32_t n_q, uint32_t n_rx, uint32_t n_miss,
+                                               bool overflow, int lane) {
     unsigned int vq = n_q, vr = n_rx, vm = n_miss, vo = overflow ? 1u : 0u;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -391,6 +416,279 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs a) {
         if (vm) atomicAdd(a.counters + 2, (unsigned long long)vm);
         if (vo) atomicOr(a.counters + 3, 1ull);
     }
+}
+
+// v1: grid-stride, one ray per lane start to finish; the wave waits for its slowest ray.
+template <int BLOCK, int STACK>
+__global__ __launch_bounds__(BLOCK) void trace_kernel_v1(TraceArgs a) {
+    __shared__ int stk[STACK * BLOCK];
+    const int lane = threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    bool overflow = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + lane; i < n; i += (uint64_t)gridDim.x * BLOCK) {
+        RayState s;
+        ray_init(a, s, a.ray_begin + i);
+        while (wants_query(a, s)) {
+            ++n_q;
+            Ray r;
+            setup_ray(r, s.pos, s.dir);
+            Trav t;
+            trav_init(t);
+            while (trav_step<BLOCK, STACK>(a, r, t, stk, lane, overflow)) {
+            }
+            shade(a, s, r, t.best, n_rx, n_miss);
+        }
+    }
+    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+}
+
+// v2: persistent waves over a global ray cursor.  Lanes whose query is finished wait
+// (masked) until THRESH lanes of the wave are waiting, then the wave shades them, refills
+// finished rays from the cursor (one atomic per wave) and starts their next queries, so a
+// wave never idles behind its slowest ray.  Results are identical to v1: the histogram is
+// order-independent and every ray follows the same arithmetic.
+template <int BLOCK, int STACK, int THRESH>
+__global__ __launch_bounds__(BLOCK) void trace_kernel_v2(TraceArgs a) {
+    __shared__ int stk[STACK * BLOCK];
+    const int lane = threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    unsigned long long* const cursor = a.counters + 4;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    bool overflow = false;
+    bool active = false;    // lane holds a ray
+    bool trav = false;      // lane is inside a closest-hit query
+    bool exhausted = false; // wave-uniform: the cursor passed n
+    RayState s;
+    Ray r;
+    Trav t;
+    trav_init(t);
+    s.depth = -1;
+    while (true) {
+        // (1) shade lanes whose query finished; a ray that will not query again retires
+        if (active && !trav) {
+            shade(a, s, r, t.best, n_rx, n_miss);
+            if (!wants_query(a, s)) active = false;
+        }
+        // (2) refill retired lanes from the global cursor, one atomic per wave
+        const unsigned long long need = __ballot(!active);
+        if (need != 0ull && !exhausted) {
+            const int cnt = __popcll(need);
+            const int leader = __ffsll((unsigned long long)need) - 1;
+            unsigned long long base = 0;
+            if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+            base = ((unsigned long long)hi << 32) | lo;
+            if (!active) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint64_t i = base + rank;
+                if (i < n) {
+                    ray_init(a, s, a.ray_begin + i);
+                    active = wants_query(a, s);
+                }
+            }
+            if (base + (unsigned long long)cnt >= n) exhausted = true;
+        }
+        // (3) start the next query of every active lane that is not traversing
+        if (active && !trav) {
+            ++n_q;
+            setup_ray(r, s.pos, s.dir);
+            trav_init(t);
+            trav = true;
+        }
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;  // every fetched ray retired without a query: fetch again
+        }
+        // (4) traverse until THRESH lanes are waiting to be shaded (or all are)
+        while (true) {
+            const unsigned long long tmask = __ballot(trav);
+            if (tmask == 0ull) break;
+            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            if (trav) trav = trav_step<BLOCK, STACK>(a, r, t, stk, lane, overflow);
+        }
+    }
+    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+}
+
+// ---- v3: v2's persistent refill loop + postponed leaves ("while-while", Aila & Laine 2009).
+// A lane that hits a leaf parks it (one pending slot; further leaves go on the stack as
+// tagged entries) and idles until enough lanes of the wave hold a leaf; then the whole
+// wave runs the triangle tests together.  Box tests use the fma form t = lo*inv - o*inv
+// (only their conservativeness matters; boxes are padded), so node steps are cheaper.
+// Stack entry: >= 0 inner node; < 0 leaf, -(first*16 + count) - 1 (count <= 15).
+struct Trav3 {
+    float best_t;
+    int best_id;
+    int best;
+    int node;   // inner node to visit, -1 = pop next
+    int sp;
+    int pf, pc; // pending leaf (first, count); pc == 0: none
+    int visits;
+};
+
+__device__ __forceinline__ int leaf_code(int first, int count) { return -(first * 16 + count) - 1; }
+
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void push3(Trav3& t, int* __restrict__ stk, int lane, int v, bool& overflow) {
+    if (t.sp < STACK) {
+        stk[t.sp * BLOCK + lane] = v;
+        ++t.sp;
+    } else {
+        overflow = true;
+    }
+}
+
+// One node step for a lane with no pending leaf and work left (node >= 0 or sp > 0).
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, bool& overflow) {
+    if (t.node < 0) {  // pop
+        --t.sp;
+        const int e = stk[t.sp * BLOCK + lane];
+        if (e >= 0) {
+            t.node = e;
+        } else {
+            const int v = -e - 1;
+            t.pf = v >> 4;
+            t.pc = v & 15;
+            return;
+        }
+    }
+    const float4* np = reinterpret_cast<const float4*>(a.nodes + t.node);
+    const float4 na = np[0];
+    const float4 nb = np[1];
+    const float4 nc = np[2];
+    const int4 nd = *reinterpret_cast<const int4*>(np + 3);
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = tn0 <= tf0 && nd.z >= 0;
+    const bool h1 = tn1 <= tf1 && nd.w >= 0;
+    const bool l0 = h0 && nd.z > 0, l1 = h1 && nd.w > 0;  // leaf children hit
+    const bool i0 = h0 && nd.z == 0, i1 = h1 && nd.w == 0;  // inner children hit
+    // leaves: nearer one parked, the other pushed
+    if (l0 && l1) {
+        const bool swap = tn1 < tn0;
+        t.pf = swap ? nd.y : nd.x;
+        t.pc = swap ? nd.w : nd.z;
+        push3<BLOCK, STACK>(t, stk, lane, swap ? leaf_code(nd.x, nd.z) : leaf_code(nd.y, nd.w), overflow);
+    } else if (l0) {
+        t.pf = nd.x;
+        t.pc = nd.z;
+    } else if (l1) {
+        t.pf = nd.y;
+        t.pc = nd.w;
+    }
+    if (i0 && i1) {
+        const bool swap = tn1 < tn0;
+        push3<BLOCK, STACK>(t, stk, lane, swap ? nd.x : nd.y, overflow);
+        t.node = swap ? nd.y : nd.x;
+    } else if (i0) {
+        t.node = nd.x;
+    } else if (i1) {
+        t.node = nd.y;
+    } else {
+        t.node = -1;
+    }
+}
+
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
+    __shared__ int stk[STACK * BLOCK];
+    const int lane = threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    unsigned long long* const cursor = a.counters + 4;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    bool overflow = false;
+    bool active = false;
+    bool trav = false;
+    bool exhausted = false;
+    RayState s;
+    Ray r;
+    Trav3 t;
+    float oix = 0.f, oiy = 0.f, oiz = 0.f;
+    s.depth = -1;
+    // every field defined: lanes that never receive a ray must not see a stale pending leaf
+    t.best_t = __builtin_huge_valf();
+    t.best_id = 0x7fffffff;
+    t.best = -1;
+    t.node = -1;
+    t.sp = 0;
+    t.pf = 0;
+    t.pc = 0;
+    t.visits = 0;
+    while (true) {
+        if (active && !trav) {
+            shade(a, s, r, t.best, n_rx, n_miss);
+            if (!wants_query(a, s)) active = false;
+        }
+        const unsigned long long need = __ballot(!active);
+        if (need != 0ull && !exhausted) {
+            const int cnt = __popcll(need);
+            const int leader = __ffsll((unsigned long long)need) - 1;
+            unsigned long long base = 0;
+            if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+            base = ((unsigned long long)hi << 32) | lo;
+            if (!active) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint64_t i = base + rank;
+                if (i < n) {
+                    ray_init(a, s, a.ray_begin + i);
+                    active = wants_query(a, s);
+                }
+            }
+            if (base + (unsigned long long)cnt >= n) exhausted = true;
+        }
+        if (active && !trav) {
+            ++n_q;
+            setup_ray(r, s.pos, s.dir);
+            oix = r.o[0] * r.inv[0];
+            oiy = r.o[1] * r.inv[1];
+            oiz = r.o[2] * r.inv[2];
+            t.best_t = __builtin_huge_valf();
+            t.best_id = 0x7fffffff;
+            t.best = -1;
+            t.node = 0;
+            t.sp = 0;
+            t.pc = 0;
+            t.pf = 0;
+            t.visits = 0;
+            trav = true;
+        }
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        while (true) {
+            if (trav && t.pc == 0 && t.node < 0 && t.sp == 0) trav = false;  // query finished
+            const bool can_node = trav && t.pc == 0;
+            const unsigned long long m_node = __ballot(can_node);
+            const unsigned long long m_leaf = __ballot(trav && t.pc > 0);
+            if ((m_node | m_leaf) == 0ull) break;
+            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+                if (can_node) node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+            } else if (trav && t.pc > 0) {
+                leaf_hits(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
+                t.pc = 0;
+            }
+        }
+    }
+    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
 }
 
 __global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __restrict__ L, float* __restrict__ R,
@@ -421,15 +719,99 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
 
 int trace_block_size() { return kBlock; }
 
+namespace {
+// Kernel variants for A/B measurement (ARX_TRACE_KERNEL, read per launch); all are
+// bit-identical in results.  Default = the fastest measured on MI355X.
+constexpr int kDefaultVariant = 0;  // 0 = v3<128, 32, 12, stack by tree depth, 5 waves/SIMD>
+
+template <typename K>
+int persistent_grid(K kernel, int block, uint64_t n_rays, int cus) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+    const uint64_t want = (n_rays + block - 1) / block;
+    const uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
+    return (int)(want < cap ? (want > 0 ? want : 1) : cap);
+}
+
+template <int BLOCK, int THRESH>
+hipError_t launch_v2(const TraceArgs& a, int cus, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
+    if (e != hipSuccess) return e;
+    auto k = trace_kernel_v2<BLOCK, kStackDepth, THRESH>;
+    const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1>
+hipError_t launch_v3(const TraceArgs& a, int cus, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
+    if (e != hipSuccess) return e;
+    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW>;
+    const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+}  // namespace
+
+int trace_variant() {
+    const char* v = getenv("ARX_TRACE_KERNEL");
+    return (v && v[0]) ? atoi(v) : kDefaultVariant;
+}
+
 int trace_grid_size(uint64_t n_rays, int device_cus) {
     const uint64_t blocks = (n_rays + kBlock - 1) / kBlock;
     const uint64_t cap = (uint64_t)(device_cus > 0 ? device_cus : 256) * 16;
     return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
 }
 
-hipError_t launch_trace(const TraceArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(trace_kernel, dim3(grid), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
+    switch (trace_variant()) {
+        case 1: {
+            const int grid = trace_grid_size(a.ray_end - a.ray_begin, cus);
+            hipLaunchKernelGGL((trace_kernel_v1<kBlock, kStackDepth>), dim3(grid), dim3(kBlock), 0, s, a);
+            return hipGetLastError();
+        }
+        case 3: return launch_v2<128, 8>(a, cus, s);
+        case 4: return launch_v2<128, 32>(a, cus, s);
+        case 5: return launch_v2<64, 16>(a, cus, s);
+        case 6: return launch_v2<256, 16>(a, cus, s);
+        case 7: return launch_v2<64, 32>(a, cus, s);
+        case 10: return launch_v3<128, 16, 32>(a, cus, s);
+        case 11: return launch_v3<128, 16, 16>(a, cus, s);
+        case 12: return launch_v3<128, 16, 48>(a, cus, s);
+        case 13: return launch_v3<128, 8, 32>(a, cus, s);
+        case 14: return launch_v3<64, 16, 32>(a, cus, s);
+        case 15: return launch_v3<128, 32, 32>(a, cus, s);
+        case 16: return launch_v3<128, 16, 8>(a, cus, s);
+        case 17: return launch_v3<128, 16, 4>(a, cus, s);
+        case 18: return launch_v3<128, 24, 12>(a, cus, s);
+        case 19: return launch_v3<128, 16, 12, 32>(a, cus, s);
+        case 20: return launch_v3<128, 16, 12, 32, 5>(a, cus, s);
+        case 21: return launch_v3<64, 16, 12, 32, 5>(a, cus, s);
+        case 22: return launch_v3<128, 16, 12, 32, 6>(a, cus, s);
+        // sweep: 1TL = THRESH T*8, LEAF_THRESH L*4
+        case 138: return launch_v3<128, 24, 8>(a, cus, s);
+        case 144: return launch_v3<128, 32, 16>(a, cus, s);
+        case 143: return launch_v3<128, 32, 12>(a, cus, s);
+        case 142: return launch_v3<128, 32, 8>(a, cus, s);
+        case 153: return launch_v3<128, 40, 12>(a, cus, s);
+        case 152: return launch_v3<128, 40, 8>(a, cus, s);
+        case 163: return launch_v3<128, 48, 12>(a, cus, s);
+        case 162: return launch_v3<128, 48, 8>(a, cus, s);
+        case 173: return launch_v3<128, 56, 12>(a, cus, s);
+        case 201: return launch_v3<128, 32, 12, 32, 5>(a, cus, s);
+        case 202: return launch_v3<64, 32, 12, 32, 5>(a, cus, s);
+        case 203: return launch_v3<256, 32, 12, 32, 5>(a, cus, s);
+        case 204: return launch_v3<64, 32, 12>(a, cus, s);
+        case 205: return launch_v3<256, 32, 12>(a, cus, s);
+        case 206: return launch_v3<128, 28, 12, 32, 5>(a, cus, s);
+        case 207: return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
+        case 2: return launch_v2<128, 16>(a, cus, s);
+        default:
+            if (a.bvh_depth < 28) return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
+            if (a.bvh_depth < 40) return launch_v3<128, 32, 12, 40, 5>(a, cus, s);
+            return launch_v3<128, 32, 12, kMaxStackDepth, 5>(a, cus, s);
+    }
 }
 
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len, double unit,

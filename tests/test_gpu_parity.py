@@ -155,6 +155,22 @@ def test_full_size_c3_properties(conference):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
 
 
+@pytest.mark.parametrize("variant", ["1", "2", "143", "207"])
+def test_kernel_variants_identical(conference, monkeypatch, variant):
+    """Every trace-kernel variant (grid-stride v1, persistent v2, postponed-leaf v3 and its
+    tunings) produces the default kernel's histogram bit for bit."""
+    s = RenderSettings(rays=(100, 100, 10), sample_rate=48000, base_power=3.62, max_bounces=16, hrtf_absorption_rate=0.5)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    monkeypatch.delenv("ARX_TRACE_KERNEL", raising=False)
+    r.render()
+    ref, q = r.get_ir(), r.stats()["queries"]
+    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
+    r.render()
+    got = r.get_ir()
+    assert r.stats()["queries"] == q
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
+
+
 def test_inverse_square_on_gpu():
     # listener on the +z (ear) axis: rays arrive through the half-spheres' domes, not through
     # the 0.058 m slot between the two halves (|z| < 0.029 in the local frame), which a
