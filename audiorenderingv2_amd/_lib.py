@@ -83,6 +83,8 @@ SIGNATURES = {
     "arx_set_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
     "arx_convolute_audio_file": (C.c_int, [_P, _F, C.c_size_t, _F, _F, _D, _D]),
     "arx_convolute_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
+    "arx_convolute_live_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
 }
 

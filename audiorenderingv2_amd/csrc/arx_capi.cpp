@@ -81,6 +81,11 @@ struct arx_renderer {
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;  // pinned
 
+    ConvPlan* conv_live = nullptr;  // mic path plan (block = live block length)
+    bool conv_live_ir_dirty = true;
+    double* d_live_in = nullptr;
+    double* d_live_out = nullptr;
+
     ConvPlan* conv = nullptr;
     bool conv_ir_dirty = true;
     float* d_conv_in = nullptr;
@@ -314,6 +319,9 @@ void arx_destroy(arx_renderer* r) {
     hipSetDevice(r->cfg.device);
     if (r->stream) hipStreamSynchronize(r->stream);
     if (r->conv) conv_plan_destroy(r->conv);
+    if (r->conv_live) conv_plan_destroy(r->conv_live);
+    hipFree(r->d_live_in);
+    hipFree(r->d_live_out);
     hipFree(r->d_nodes);
     hipFree(r->d_tris);
     hipFree(r->d_hist);
@@ -479,6 +487,7 @@ arx_status arx_finalize_ir(arx_renderer* r) {
     ARX_HIP(launch_finalize_ir((const long long*)r->hist(), r->d_ir, r->d_ir + r->ir_len, r->ir_len, unit,
                                r->cfg.is_mono, r->stream));
     r->conv_ir_dirty = true;
+    r->conv_live_ir_dirty = true;
     return ARX_OK;
 }
 
@@ -556,6 +565,7 @@ arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right
     ARX_HIP(hipMemcpyAsync(r->d_ir + r->ir_len, h_right, ir_len * sizeof(float), hipMemcpyHostToDevice, r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));
     r->conv_ir_dirty = true;
+    r->conv_live_ir_dirty = true;
     return ARX_OK;
 }
 
@@ -625,6 +635,54 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
     }
     hipEventDestroy(p0);
     hipEventDestroy(p1);
+    return ARX_OK;
+}
+
+arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t n_in, double* d_out) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n_in > (size_t)r->ir_len)  // the reference copies the block into an ir_len buffer (AudioRenderer.cpp:600-603)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "live block of %zu samples exceeds ir_len %d", n_in, r->ir_len);
+    if ((n_in > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    const int32_t block = (int32_t)std::max<size_t>(n_in, 1);
+    if (!r->conv_live || conv_plan_block(r->conv_live) < block) {
+        if (r->conv_live) conv_plan_destroy(r->conv_live);
+        char err[256] = {0};
+        // plan block = the longest block seen, rounded up to 4096 frames (main.cpp:37)
+        const int32_t b = std::min<int32_t>(r->ir_len, std::max<int32_t>(4096, block));
+        r->conv_live = conv_plan_create(r->ir_len, b, r->cfg.device, err, sizeof(err));
+        if (!r->conv_live) return fail(ARX_ERR_INTERNAL, "live convolution plan: %s", err);
+        r->conv_live_ir_dirty = true;
+    }
+    if (r->conv_live_ir_dirty) {
+        ARX_HIP(conv_set_ir(r->conv_live, r->d_ir, r->d_ir + r->ir_len, r->stream));
+        r->conv_live_ir_dirty = false;
+    }
+    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
+    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t in_bytes, double* h_out,
+                                    size_t out_len) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    const size_t n_in = in_bytes / sizeof(double);
+    if (out_len != 2 * (size_t)r->ir_len)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "output must hold 2*ir_len = %zu doubles", 2 * (size_t)r->ir_len);
+    if ((n_in > 0 && !h_in) || !h_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    if (n_in > (size_t)r->ir_len)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "live block of %zu samples exceeds ir_len %d", n_in, r->ir_len);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (!r->d_live_in) {
+        ARX_HIP(hipMalloc(&r->d_live_in, (size_t)r->ir_len * sizeof(double)));
+        ARX_HIP(hipMalloc(&r->d_live_out, 2 * (size_t)r->ir_len * sizeof(double)));
+    }
+    if (n_in > 0) ARX_HIP(hipMemcpyAsync(r->d_live_in, h_in, n_in * sizeof(double), hipMemcpyHostToDevice, r->stream));
+    arx_status st = arx_convolute_live_device(r, r->d_live_in, n_in, r->d_live_out);
+    if (st != ARX_OK) return st;
+    ARX_HIP(hipMemcpyAsync(h_out, r->d_live_out, out_len * sizeof(double), hipMemcpyDeviceToHost, r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
     return ARX_OK;
 }
 

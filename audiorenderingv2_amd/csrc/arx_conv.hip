@@ -158,6 +158,9 @@ struct PassArgs {
     float* out_r;
     int64_t len;
     double scale;
+    const double* in_d;  // live block input (f64)
+    int64_t n_in;        // live block length (<= block length of the plan)
+    double* out_d;       // live output, interleaved L/R, 2*n doubles
 };
 
 // Pass A: forward column FFTs.  mode 0: batch = block pair p; mode 1: batch = IR channel c.
@@ -183,6 +186,8 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
                 if (b0 < a.n_blocks) x.x = (double)a.in[b0 * a.sr + idx];
                 if (b1 < a.n_blocks) x.y = (double)a.in[b1 * a.sr + idx];
             }
+        } else if (MODE == 2) {  // live block (f64 samples), zero padded
+            if (idx < a.n_in) x.x = a.in_d[idx];
         } else {
             if (idx < a.n) x.x = (double)(batch == 0 ? a.ir_l : a.ir_r)[idx];
         }
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
     __syncthreads();
     lds_fft(buf, a.N1, a.lg1, -1, t, per, a.tw, a.M);
     // twiddle W_M^(n2*k1) and store transposed: S[k1*N2 + n2]
-    double2* dst = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
+    double2* dst = (MODE != 1) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
     for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
         const int c = i % tc, k1 = i / tc;
         const int64_t e = (int64_t)(n2_0 + c) * k1;
@@ -289,6 +294,21 @@ __global__ __launch_bounds__(kThreads) void pass_d(PassArgs a) {
         acc += v;
     }
     (ch == 0 ? a.out_l : a.out_r)[j] = (float)(acc * a.scale);
+}
+
+// Live pass D (convoluteLiveInput, AudioRenderer.cpp:623-644): the single block's circular
+// length-n convolution (lin[i] + lin[i+n]) for i in [0, n), scaled n/(M*(n/2)) (Z2D x n then
+// normalizeBuffers' /(ir_len/2)) and zipped L/R (d_zipArrays, kernels.cu:469-479), in f64.
+__global__ __launch_bounds__(kThreads) void pass_d_live(PassArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= a.n) return;
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        const double* y = a.Y + ch * a.ylen;
+        double v = y[i];
+        if (i + a.n < a.ylen) v += y[i + a.n];
+        a.out_d[2 * i + ch] = v * a.scale;
+    }
 }
 
 int ilog2(int64_t v) {
@@ -414,6 +434,40 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+int32_t conv_plan_block(const ConvPlan* p) { return p ? p->sr : 0; }
+
+hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s) {
+    if (n_in < 0 || n_in > p->sr) return hipErrorInvalidValue;
+    const int64_t ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    if (p->pairs_cap < 1) {
+        hipFree(p->d_S);
+        hipFree(p->d_Y);
+        p->d_S = nullptr;
+        p->d_Y = nullptr;
+        hipError_t e = hipMalloc(&p->d_S, (size_t)3 * p->M * sizeof(double2));
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&p->d_Y, (size_t)2 * 2 * ylen * sizeof(double));
+        if (e != hipSuccess) return e;
+        p->pairs_cap = 1;
+    }
+    PassArgs a = base_args(p);
+    a.in_d = d_in;
+    a.n_in = n_in;
+    a.S = p->d_S;
+    a.Y = p->d_Y;
+    a.n_blocks = 1;
+    a.n_pairs = 1;
+    a.out_d = d_out_interleaved;
+    a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
+    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
+    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
+    hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, 1), dim3(kThreads), lds_b, s, a);
+    hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
+    hipLaunchKernelGGL(pass_d_live, dim3((unsigned)((p->n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -29,5 +29,10 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
                     hipStream_t s);
 const char* conv_plan_describe(const ConvPlan* p);
+// Live (mic) block: plans created with sample_rate = block length.  One block of n_in <= block
+// f64 samples, circular length-ir_len convolution with both IR spectra, / (ir_len/2), zipped
+// L/R into 2*ir_len doubles (AudioRenderer.cpp:593-651, kernels.cu:345-377, 450-487).
+hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s);
+int32_t conv_plan_block(const ConvPlan* p);
 
 }  // namespace arx

@@ -180,6 +180,20 @@ class AudioRenderer:
                                              C.byref(pms)))
         return L, R, cms.value, pms.value
 
+    def convoluteLiveInput(self, block: np.ndarray, circular_buffer=None) -> np.ndarray:
+        """AudioRenderer::convoluteLiveInput (AudioRenderer.cpp:593-661): one f64 mic block ->
+        2*ir_len interleaved doubles, added into circular_buffer (CircularBuffer::add) if given."""
+        x = np.ascontiguousarray(block, np.float64)
+        out = np.empty(2 * self.ir_length, np.float64)
+        D = C.POINTER(C.c_double)
+        check(lib().arx_convolute_live_block(self._h, x.ctypes.data_as(D), x.nbytes, out.ctypes.data_as(D), out.size))
+        if circular_buffer is not None:
+            circular_buffer.add(out)
+        return out
+
+    def convolute_live_device(self, d_in: int, n_in: int, d_out: int) -> None:
+        check(lib().arx_convolute_live_device(self._h, C.c_void_p(d_in), n_in, C.c_void_p(d_out)))
+
     def convolute_device(self, d_in: int, n_frames: int, d_out_left: int, d_out_right: int) -> None:
         check(lib().arx_convolute_device(self._h, C.c_void_p(d_in), n_frames, C.c_void_p(d_out_left),
                                          C.c_void_p(d_out_right)))

@@ -147,6 +147,17 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
                                 float* d_out_right);
 
+/* AudioRenderer::convoluteLiveInput (AudioRenderer.h:29; AudioRenderer.cpp:593-661) over
+ * convoluteFromLiveInput (kernels.cu:345-377) minus the CircularBuffer (which stays with the
+ * caller, include/arx_circular_buffer.hpp): one mic block of in_bytes/8 f64 samples (<= ir_len),
+ * zero padded to ir_len, circularly convolved with each IR in f64, divided by (ir_len/2) and
+ * zipped L/R into h_out[2*ir_len] (out_len must be 2*ir_len).  IR spectra are cached between
+ * callbacks (the reference re-plans and re-transforms them every callback). */
+arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t in_bytes, double* h_out,
+                                    size_t out_len);
+/* Same on device buffers (n_in f64 samples in, 2*ir_len f64 out), no host synchronisation. */
+arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t n_in, double* d_out);
+
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);
