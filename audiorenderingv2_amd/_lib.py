@@ -44,9 +44,35 @@ class ArxStats(C.Structure):
     ]
 
 
+PATH_MAX = 1024
+NAME_MAX = 128
+MAX_MATERIALS = 256
+
+
+class ArxAppConfig(C.Structure):
+    """arx_app_config: Context::loadContext's parameters (Context.cpp:15-164)."""
+    _fields_ = [
+        ("initial_volume", C.c_float),
+        ("ir_length_in_seconds", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+        ("write_first_ir_to_file", C.c_int32), ("write_first_output_to_file", C.c_int32),
+        ("re_render_distance_threshold", C.c_float), ("re_render_angle_threshold", C.c_float),
+        ("mono", C.c_int32),
+        ("scene_file_path", C.c_char * PATH_MAX), ("audio_file_path", C.c_char * PATH_MAX),
+        ("materials_file_path", C.c_char * PATH_MAX),
+        ("initial_receiver_pos", C.c_float * 3), ("initial_emitter_pos", C.c_float * 3),
+        ("base_power", C.c_float), ("rays", C.c_float * 3), ("ray_energy_threshold", C.c_float),
+        ("ray_max_bounces", C.c_uint32), ("hrtf_absorption_rate", C.c_float),
+        ("n_materials", C.c_int32),
+        ("material_names", (C.c_char * NAME_MAX) * MAX_MATERIALS),
+        ("material_absorption", C.c_float * MAX_MATERIALS),
+    ]
+
+
 _P = C.c_void_p
 _F = C.POINTER(C.c_float)
 _D = C.POINTER(C.c_double)
+_I64 = C.POINTER(C.c_int64)
+_I32 = C.POINTER(C.c_int32)
 
 # name -> (restype, argtypes); must cover every function declared in include/arx.h
 SIGNATURES = {
@@ -86,6 +112,21 @@ SIGNATURES = {
     "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
     "arx_convolute_live_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
+    # input formats (host only)
+    "arx_model_load_obj": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(_P)]),
+    "arx_model_free": (None, [_P]),
+    "arx_model_mesh_count": (C.c_int64, [_P]),
+    "arx_model_material_count": (C.c_int64, [_P]),
+    "arx_model_info": (None, [_P, _I64, _I64, _I64]),
+    "arx_model_mesh": (C.c_int, [_P, C.c_int64, C.POINTER(C.c_char_p), C.POINTER(_F), _I64,
+                                 C.POINTER(_I32), _I64]),
+    "arx_model_triangle_count": (C.c_int64, [_P]),
+    "arx_model_flatten": (C.c_int, [_P, C.POINTER(C.c_char_p), _F, C.c_size_t, _F, _F]),
+    "arx_wav_load": (C.c_int, [C.c_char_p, C.POINTER(_F), _I32, _I64, _I32, _I32]),
+    "arx_free": (None, [_P]),
+    "arx_default_app_config": (None, [C.POINTER(ArxAppConfig)]),
+    "arx_parse_app_config": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(ArxAppConfig)]),
+    "arx_load_app_config": (C.c_int, [C.c_char_p, C.POINTER(ArxAppConfig)]),
 }
 
 _lib = None

@@ -48,6 +48,9 @@ arx_status fail(arx_status s, const char* fmt, ...) {
 
 }  // namespace
 
+// shared with arx_io.cpp so the loaders report through arx_last_error()
+void arx_set_last_error(const std::string& m) { g_last_error = m; }
+
 struct arx_renderer {
     arx_config cfg;
     int32_t ir_len = 0;

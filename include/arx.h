@@ -162,6 +162,70 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);
 
+/* ---- Input formats (host only, no device needed) ------------------------------------------ */
+
+/* OBJ scene / receiver model: tinyobj v2.0.0 LoadObj with triangulation (R/prebuild/common/
+ * 3rdParty/tiny_obj_loader.h:2095-2600) then one mesh per (shape, material id ascending) with
+ * (v,n,t) vertex dedup -- loadOBJ (R/prebuild/obj_raytracer/OptixModel.cpp:75-151).
+ * mtl_dir NULL = the OBJ's directory (loadOBJ :79).  first_shape_only + forced_name give
+ * HalfSphere + place_receiver_half (HalfSphere.cpp:3-31, OptixModel.cpp:197-220): pass
+ * mtl_dir = path up to (excluding) the last '/', forced_name "receiver_left"/"receiver_right".
+ * Fails (ARX_ERR_IO) when the OBJ has no materials, like the reference's throw. */
+typedef struct arx_model arx_model;
+arx_status arx_model_load_obj(const char* path, const char* mtl_dir, int first_shape_only,
+                              const char* forced_name, arx_model** out);
+void arx_model_free(arx_model* m);
+int64_t arx_model_mesh_count(const arx_model* m);
+int64_t arx_model_material_count(const arx_model* m);
+/* tinyobj's shapes.size(), materials.size(), attrib.vertices.size()/3 */
+void arx_model_info(const arx_model* m, int64_t* n_shapes, int64_t* n_materials, int64_t* n_positions);
+/* Mesh i: TriangleMesh {material_name, vertex, index} (OptixModel.h); pointers live until free. */
+arx_status arx_model_mesh(const arx_model* m, int64_t i, const char** name, const float** vertices,
+                          int64_t* n_vertices, const int32_t** indices, int64_t* n_triangles);
+int64_t arx_model_triangle_count(const arx_model* m);
+/* Triangle soup for arx_set_scene (9 floats per triangle, meshes in model order) with
+ * getMaterialAbsorption per mesh name (AudioRenderer.cpp:34-56, :455); tri_absorption may be NULL. */
+arx_status arx_model_flatten(const arx_model* m, const char* const* names, const float* absorption,
+                             size_t n_materials, float* tri_vertices, float* tri_absorption);
+
+/* WAV: AudioFile<float>::load / decodeWaveFile (R/prebuild/obj_raytracer/AudioFile.h:502-640,
+ * sample conversion :1242-1269): PCM 8/16/24/32-bit and IEEE float 32.  *samples is malloc'd,
+ * channel-major (channels x frames, like AudioFile::samples); release with arx_free. */
+arx_status arx_wav_load(const char* path, float** samples, int32_t* channels, int64_t* frames,
+                        int32_t* sample_rate, int32_t* bit_depth);
+void arx_free(void* p);
+
+/* config.json: Context::loadContext's parameters (R/prebuild/obj_raytracer/Context.cpp:15-164)
+ * with its defaults and rounding (unsigned fields and both re_render thresholds and
+ * hrtf_absorption_rate are round()ed), parsed with cJSON 1.7.16 semantics (case-insensitive
+ * keys, first duplicate wins, trailing text ignored). */
+#define ARX_PATH_MAX 1024
+#define ARX_NAME_MAX 128
+#define ARX_MAX_MATERIALS 256
+typedef struct arx_app_config {
+    float initial_volume;
+    uint32_t ir_length_in_seconds, width, height;
+    int32_t write_first_ir_to_file, write_first_output_to_file;
+    float re_render_distance_threshold, re_render_angle_threshold;
+    int32_t mono;
+    char scene_file_path[ARX_PATH_MAX];
+    char audio_file_path[ARX_PATH_MAX];     /* "" = live mic input, sample rate 44100 */
+    char materials_file_path[ARX_PATH_MAX];
+    float initial_receiver_pos[3];
+    float initial_emitter_pos[3];
+    float base_power;
+    float rays[3];                          /* gdt::vec3f; launch dims are int(rays) (LaunchParams.h:24) */
+    float ray_energy_threshold;
+    uint32_t ray_max_bounces;
+    float hrtf_absorption_rate;
+    int32_t n_materials;
+    char material_names[ARX_MAX_MATERIALS][ARX_NAME_MAX];
+    float material_absorption[ARX_MAX_MATERIALS];
+} arx_app_config;
+void arx_default_app_config(arx_app_config* c);
+arx_status arx_parse_app_config(const char* text, size_t len, arx_app_config* c);
+arx_status arx_load_app_config(const char* path, arx_app_config* c);
+
 #ifdef __cplusplus
 }
 #endif
