@@ -111,6 +111,7 @@ SIGNATURES = {
     "arx_convolute_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
     "arx_convolute_live_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "arx_prepare_ir_spectra": (C.c_int, [_P, C.c_int]),
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     # input formats (host only)
     "arx_model_load_obj": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(_P)]),
@@ -124,6 +125,9 @@ SIGNATURES = {
     "arx_model_flatten": (C.c_int, [_P, C.POINTER(C.c_char_p), _F, C.c_size_t, _F, _F]),
     "arx_wav_load": (C.c_int, [C.c_char_p, C.POINTER(_F), _I32, _I64, _I32, _I32]),
     "arx_free": (None, [_P]),
+    "arx_wav_save": (C.c_int, [C.c_char_p, _F, C.c_int32, C.c_int64, C.c_int32, C.c_int32]),
+    "arx_normalize_min_max": (C.c_int, [_F, C.c_size_t]),
+    "arx_write_float_lines": (C.c_int, [C.c_char_p, _F, C.c_size_t]),
     "arx_default_app_config": (None, [C.POINTER(ArxAppConfig)]),
     "arx_parse_app_config": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(ArxAppConfig)]),
     "arx_load_app_config": (C.c_int, [C.c_char_p, C.POINTER(ArxAppConfig)]),

@@ -586,6 +586,32 @@ static arx_status ensure_conv(arx_renderer* r) {
     return ARX_OK;
 }
 
+static arx_status ensure_conv_live(arx_renderer* r, int32_t block) {
+    if (!r->conv_live || conv_plan_block(r->conv_live) < block) {
+        if (r->conv_live) conv_plan_destroy(r->conv_live);
+        char err[256] = {0};
+        // plan block = the longest block seen, rounded up to 4096 frames (main.cpp:37)
+        const int32_t b = std::min<int32_t>(r->ir_len, std::max<int32_t>(4096, block));
+        r->conv_live = conv_plan_create(r->ir_len, b, r->cfg.device, err, sizeof(err));
+        if (!r->conv_live) return fail(ARX_ERR_INTERNAL, "live convolution plan: %s", err);
+        r->conv_live_ir_dirty = true;
+    }
+    if (r->conv_live_ir_dirty) {
+        ARX_HIP(conv_set_ir(r->conv_live, r->d_ir, r->d_ir + r->ir_len, r->stream));
+        r->conv_live_ir_dirty = false;
+    }
+    return ARX_OK;
+}
+
+arx_status arx_prepare_ir_spectra(arx_renderer* r, int which) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = ARX_OK;
+    if (which & 1) st = ensure_conv(r);
+    if (st == ARX_OK && (which & 2)) st = ensure_conv_live(r, 1);
+    return st;
+}
+
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
                                 float* d_out_right) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
@@ -647,20 +673,8 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
         return fail(ARX_ERR_INVALID_ARGUMENT, "live block of %zu samples exceeds ir_len %d", n_in, r->ir_len);
     if ((n_in > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    const int32_t block = (int32_t)std::max<size_t>(n_in, 1);
-    if (!r->conv_live || conv_plan_block(r->conv_live) < block) {
-        if (r->conv_live) conv_plan_destroy(r->conv_live);
-        char err[256] = {0};
-        // plan block = the longest block seen, rounded up to 4096 frames (main.cpp:37)
-        const int32_t b = std::min<int32_t>(r->ir_len, std::max<int32_t>(4096, block));
-        r->conv_live = conv_plan_create(r->ir_len, b, r->cfg.device, err, sizeof(err));
-        if (!r->conv_live) return fail(ARX_ERR_INTERNAL, "live convolution plan: %s", err);
-        r->conv_live_ir_dirty = true;
-    }
-    if (r->conv_live_ir_dirty) {
-        ARX_HIP(conv_set_ir(r->conv_live, r->d_ir, r->d_ir + r->ir_len, r->stream));
-        r->conv_live_ir_dirty = false;
-    }
+    arx_status st = ensure_conv_live(r, (int32_t)std::max<size_t>(n_in, 1));
+    if (st != ARX_OK) return st;
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
     ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
     ARX_HIP(hipEventRecord(r->ev1, r->stream));

@@ -694,6 +694,102 @@ arx_status arx_wav_load(const char* path, float** samples, int32_t* channels, in
 
 void arx_free(void* p) { std::free(p); }
 
+// AudioFile<float>::saveToWaveFile (AudioFile.h:842-955): 32-bit is always IEEE float with an
+// 18-byte fmt chunk; 8/16-bit clamp to [-1,1]; 24-bit scales without clamping.
+arx_status arx_wav_save(const char* path, const float* samples, int32_t channels, int64_t frames,
+                        int32_t sample_rate, int32_t bit_depth) {
+    if (!path || (!samples && frames > 0) || channels < 1 || channels > 128 || frames < 0)
+        return io_fail(ARX_ERR_INVALID_ARGUMENT, "bad WAV parameters");
+    if (bit_depth != 8 && bit_depth != 16 && bit_depth != 24 && bit_depth != 32)
+        return io_fail(ARX_ERR_INVALID_ARGUMENT, "unsupported bit depth");
+    const int64_t data_size64 = frames * channels * (bit_depth / 8);
+    if (data_size64 > 0x7fffff00LL) return io_fail(ARX_ERR_INVALID_ARGUMENT, "WAV data exceeds 2 GiB");
+    const int32_t data_size = (int32_t)data_size64;
+    const bool ieee = bit_depth == 32;
+    const int32_t fmt_size = ieee ? 18 : 16;
+    std::vector<uint8_t> f;
+    f.reserve((size_t)data_size + 64);
+    auto str = [&](const char* s) { f.insert(f.end(), s, s + 4); };
+    auto i32 = [&](int32_t v) {
+        for (int b = 0; b < 4; ++b) f.push_back((uint8_t)(((uint32_t)v >> (8 * b)) & 0xFF));
+    };
+    auto i16 = [&](int16_t v) {
+        f.push_back((uint8_t)(v & 0xFF));
+        f.push_back((uint8_t)(((uint16_t)v >> 8) & 0xFF));
+    };
+    str("RIFF");
+    i32(4 + fmt_size + 8 + 8 + data_size);
+    str("WAVE");
+    str("fmt ");
+    i32(fmt_size);
+    i16(ieee ? 3 : 1);
+    i16((int16_t)channels);
+    i32(sample_rate);
+    i32((int32_t)(((int64_t)channels * sample_rate * bit_depth) / 8));
+    i16((int16_t)(channels * (bit_depth / 8)));
+    i16((int16_t)bit_depth);
+    if (ieee) i16(0);
+    str("data");
+    i32(data_size);
+    for (int64_t i = 0; i < frames; ++i) {
+        for (int c = 0; c < channels; ++c) {
+            float s = samples[(size_t)c * (size_t)frames + (size_t)i];
+            if (bit_depth == 8) {
+                s = std::max(std::min(s, 1.0f), -1.0f);
+                s = (float)(((double)s + 1.) / 2.);
+                f.push_back((uint8_t)((double)s * 255.));
+            } else if (bit_depth == 16) {
+                s = std::max(std::min(s, 1.0f), -1.0f);
+                i16((int16_t)((double)s * 32767.));
+            } else if (bit_depth == 24) {
+                const int32_t x = (int32_t)(s * 8388608.0f);
+                f.push_back((uint8_t)(x & 0xFF));
+                f.push_back((uint8_t)((x >> 8) & 0xFF));
+                f.push_back((uint8_t)((x >> 16) & 0xFF));
+            } else {
+                int32_t x;
+                std::memcpy(&x, &s, 4);
+                i32(x);
+            }
+        }
+    }
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return io_fail(ARX_ERR_IO, std::string("cannot write ") + path);
+    const size_t w = std::fwrite(f.data(), 1, f.size(), fp);
+    const bool ok = (std::fclose(fp) == 0) && w == f.size();
+    return ok ? ARX_OK : io_fail(ARX_ERR_IO, std::string("short write to ") + path);
+}
+
+// normalizeToRangeMinusOneToOne (R/prebuild/obj_raytracer/main.cpp:628-651): f32 min-max map
+// to [-1, 1]; constant input is an error (the reference throws).
+arx_status arx_normalize_min_max(float* data, size_t n) {
+    if (n == 0) return ARX_OK;
+    if (!data) return io_fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    // std::min_element / max_element: first minimum / maximum under operator<
+    float lo = data[0], hi = data[0];
+    for (size_t i = 1; i < n; ++i) {
+        if (data[i] < lo) lo = data[i];
+        if (hi < data[i]) hi = data[i];
+    }
+    if (lo == hi) return io_fail(ARX_ERR_INVALID_ARGUMENT, "Cannot normalize: all elements in the vector are the same.");
+    const float range = hi - lo;
+    for (size_t i = 0; i < n; ++i) data[i] = 2.0f * ((data[i] - lo) / range) - 1.0f;
+    return ARX_OK;
+}
+
+// The text dumps of AudioRenderer.cpp:525-567 / :720-744: one value per line through
+// std::ostream's default float formatting (%g, precision 6).
+arx_status arx_write_float_lines(const char* path, const float* data, size_t n) {
+    if (!path || (!data && n)) return io_fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    FILE* fp = std::fopen(path, "w");
+    if (!fp) return io_fail(ARX_ERR_IO, std::string("cannot write ") + path);
+    std::vector<char> buf(1 << 20);
+    std::setvbuf(fp, buf.data(), _IOFBF, buf.size());
+    for (size_t i = 0; i < n; ++i) std::fprintf(fp, "%g\n", (double)data[i]);
+    const bool ok = std::fclose(fp) == 0;
+    return ok ? ARX_OK : io_fail(ARX_ERR_IO, std::string("write failed: ") + path);
+}
+
 }  // extern "C"
 
 // ----------------------------------------------------------------- JSON ----

@@ -133,6 +133,31 @@ def load_wav(path: str) -> Wav:
     return Wav(data.reshape(ch.value, n.value), sr.value, bits.value)
 
 
+def save_wav(path: str, samples: np.ndarray, sample_rate: int, bit_depth: int = 16) -> None:
+    """AudioFile<float>::save (AudioFile.h:842-955); samples (channels, frames) or (frames,)."""
+    x = np.ascontiguousarray(np.atleast_2d(samples), np.float32)
+    check(lib().arx_wav_save(os.fsencode(path), x.ctypes.data_as(C.POINTER(C.c_float)), x.shape[0], x.shape[1],
+                             int(sample_rate), int(bit_depth)))
+
+
+def normalize_to_range_minus_one_to_one(x: np.ndarray) -> np.ndarray:
+    """normalizeToRangeMinusOneToOne (main.cpp:628-651) on a copy; raises on constant input."""
+    y = np.array(x, np.float32, copy=True).reshape(-1)
+    check(lib().arx_normalize_min_max(y.ctypes.data_as(C.POINTER(C.c_float)), y.size))
+    return y
+
+
+def write_float_lines(path: str, data: np.ndarray) -> None:
+    """One value per line in std::ostream's default format (AudioRenderer.cpp:552-556)."""
+    x = np.ascontiguousarray(data, np.float32).reshape(-1)
+    check(lib().arx_write_float_lines(os.fsencode(path), x.ctypes.data_as(C.POINTER(C.c_float)), x.size))
+
+
+def read_float_lines(path: str) -> np.ndarray:
+    """Reader for the text dumps (what R/utils/*.py plot)."""
+    return np.loadtxt(path, dtype=np.float64, ndmin=1).astype(np.float32)
+
+
 @dataclass
 class AppConfig:
     """Context::loadContext's parameters with the reference's defaults (Context.cpp:19-119)."""

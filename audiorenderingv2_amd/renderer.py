@@ -8,11 +8,14 @@ call goes through libarx.so's C ABI (include/arx.h); there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
 
 from ._lib import ArxConfig, ArxStats, check, fptr, lib
+from .formats import write_float_lines
 from .scene import Scene
 
 
@@ -125,10 +128,36 @@ class AudioRenderer:
 
     # -- render ------------------------------------------------------------------
     def render(self) -> float:
-        """AudioRenderer::render (AudioRenderer.cpp:489-523); returns the trace kernel's ms."""
+        """AudioRenderer::render (AudioRenderer.cpp:489-523); returns the trace kernel's ms.
+        With the write-IR flag set, dumps the IR once like :525-567 and clears the flag."""
         ms = C.c_double()
         check(lib().arx_render(self._h, C.byref(ms)))
+        if self.write_ir_to_file_flag:
+            L, R = self.get_ir()
+            lp, rp = "output_ir_left.txt", "output_ir_right.txt"
+            if self.experimentation:
+                stamp = time.time_ns()
+                lp = os.path.join("experimentation", f"output_ir_left_{stamp}.txt")
+                rp = os.path.join("experimentation", f"output_ir_right_{stamp}.txt")
+            write_float_lines(os.path.join(self.output_dir, lp), L)
+            write_float_lines(os.path.join(self.output_dir, rp), R)
+            self.write_ir_to_file_flag = False
         return ms.value
+
+    # -- text dumps (AudioRenderer.cpp:525-567, 720-744; setters :780-788) -----------
+    write_ir_to_file_flag = False
+    write_output_to_file_flag = False
+    experimentation = False
+    output_dir = "."
+
+    def set_write_ir_to_file_flag(self, value: bool) -> None:
+        self.write_ir_to_file_flag = bool(value)
+
+    def set_write_output_to_file_flag(self, value: bool) -> None:
+        self.write_output_to_file_flag = bool(value)
+
+    def enable_experimentation(self) -> None:
+        self.experimentation = True
 
     def clear_histogram(self) -> None:
         check(lib().arx_clear_histogram(self._h))
@@ -178,6 +207,10 @@ class AudioRenderer:
         cms, pms = C.c_double(), C.c_double()
         check(lib().arx_convolute_audio_file(self._h, fptr(x), x.nbytes, fptr(L), fptr(R), C.byref(cms),
                                              C.byref(pms)))
+        if self.write_output_to_file_flag:
+            write_float_lines(os.path.join(self.output_dir, "output_convolute_left.txt"), L)
+            write_float_lines(os.path.join(self.output_dir, "output_convolute_right.txt"), R)
+            self.write_output_to_file_flag = False
         return L, R, cms.value, pms.value
 
     def convoluteLiveInput(self, block: np.ndarray, circular_buffer=None) -> np.ndarray:
@@ -190,6 +223,10 @@ class AudioRenderer:
         if circular_buffer is not None:
             circular_buffer.add(out)
         return out
+
+    def prepare_ir_spectra(self, file: bool = True, live: bool = False) -> None:
+        """Recompute the cached IR spectra now (async) rather than in the next convolution."""
+        check(lib().arx_prepare_ir_spectra(self._h, (1 if file else 0) | (2 if live else 0)))
 
     def convolute_live_device(self, d_in: int, n_in: int, d_out: int) -> None:
         check(lib().arx_convolute_live_device(self._h, C.c_void_p(d_in), n_in, C.c_void_p(d_out)))

@@ -111,6 +111,39 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def moving_listener(r, D, dev, stream, hist, ray_begin, ray_end, frames: int) -> dict:
+    """the listener moves 0.05 m/frame along +x with yaw += 1 deg/frame.
+    Frame latency = host wall time of: receiver re-placement (host transform + sub-tree BVH
+    rebuild + upload, no scene rebuild) -> clear -> trace this rank's shard -> RCCL all-reduce
+    -> finalize IR -> new IR spectra for the file and live convolution paths, synchronised.
+    The reference instead re-places the receiver and rebuilds the whole GAS and pipeline
+    (OptixModel.cpp:153-257, AudioRenderer.cpp:466-486, 790-798).  p50/p99 are max over ranks."""
+    import torch
+
+    from audiorenderingv2_amd.scene import CONFERENCE_LISTENER
+
+    x0, y0, z0 = CONFERENCE_LISTENER
+    lat = []
+    for k in range(frames + 3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r.setSphereCenterInOptix((x0 + 0.05 * k, y0, z0), float(k % 360))
+        r.clear_histogram()
+        r.trace_rays(ray_begin, ray_end)
+        D.allreduce_histogram(hist)
+        r.finalize_ir()
+        r.prepare_ir_spectra(file=True, live=True)
+        stream.synchronize()
+        if k >= 3:  # first frames warm the receiver rebuild path
+            lat.append((time.perf_counter() - t0) * 1e3)
+    a = np.array(lat)
+    p50 = D.max_over_ranks(float(np.percentile(a, 50)), dev)
+    p99 = D.max_over_ranks(float(np.percentile(a, 99)), dev)
+    return {"frames": frames, "p50_ms": p50, "p99_ms": p99, "max_ms": D.max_over_ranks(float(a.max()), dev),
+            "budget_ms": 1000.0 / 60.0,
+            "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + all-reduce + finalize + IR spectra"}
+
+
 def load_traffic() -> dict | None:
     path = os.path.join(REPO, "profiles", "trace_traffic.json")
     if os.path.exists(path):
@@ -127,6 +160,8 @@ def main(argv=None) -> int:
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c5-frames", type=int, default=600,
+                    help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     args = ap.parse_args(argv)
 
     import torch
@@ -207,6 +242,7 @@ def main(argv=None) -> int:
 
     value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
+    moving = moving_listener(r, D, dev, stream, hist, b, e, args.c5_frames) if args.c5_frames > 0 else None
     bpb = bytes_per_bounce(n_tris)
     achieved = q_rank * bpb / (trace_ms * 1e-3) / 1e9
     traffic = load_traffic()
@@ -260,6 +296,8 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
         },
     }
+    if moving is not None:
+        result["moving_listener"] = moving
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, receiver, wl, total_rays, args.cpu_baseline_seconds)
     if rank == 0:

@@ -157,6 +157,10 @@ arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t 
                                     size_t out_len);
 /* Same on device buffers (n_in f64 samples in, 2*ir_len f64 out), no host synchronisation. */
 arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t n_in, double* d_out);
+/* Recompute the cached IR spectra now (async on the renderer's stream) instead of lazily in the
+ * next convolution: which = 1 file path, 2 live path, 3 both.  Lets a moving-listener frame
+ * (re-trace + reduce + new spectra) finish before audio needs it. */
+arx_status arx_prepare_ir_spectra(arx_renderer* r, int which);
 
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
@@ -194,6 +198,18 @@ arx_status arx_model_flatten(const arx_model* m, const char* const* names, const
 arx_status arx_wav_load(const char* path, float** samples, int32_t* channels, int64_t* frames,
                         int32_t* sample_rate, int32_t* bit_depth);
 void arx_free(void* p);
+
+/* ---- Output formats (host only) ------------------------------------------------------------ */
+
+/* AudioFile<float>::save as export_audio uses it (main.cpp:709-716; AudioFile.h:842-955):
+ * samples channel-major; 32-bit is written as IEEE float, 8/16-bit are clamped to [-1, 1]. */
+arx_status arx_wav_save(const char* path, const float* samples, int32_t channels, int64_t frames,
+                        int32_t sample_rate, int32_t bit_depth);
+/* normalizeToRangeMinusOneToOne (main.cpp:628-651), in place; constant input -> INVALID_ARGUMENT. */
+arx_status arx_normalize_min_max(float* data, size_t n);
+/* One value per line, std::ostream default float format -- the output_ir_{left,right}.txt and
+ * output_convolute_{left,right}.txt dumps (AudioRenderer.cpp:525-567, 720-744). */
+arx_status arx_write_float_lines(const char* path, const float* data, size_t n);
 
 /* config.json: Context::loadContext's parameters (R/prebuild/obj_raytracer/Context.cpp:15-164)
  * with its defaults and rounding (unsigned fields and both re_render thresholds and

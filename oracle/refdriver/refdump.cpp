@@ -236,6 +236,36 @@ int cmd_config(const std::string& path) {
     return 0;
 }
 
+std::vector<float> read_raw(const std::string& path, size_t n) {
+    std::vector<float> v(n);
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f || std::fread(v.data(), sizeof(float), n, f) != n) v.clear();
+    if (f) std::fclose(f);
+    return v;
+}
+
+// AudioFile<float>::save of a channel-major raw f32 buffer (export_audio, main.cpp:709-716)
+int cmd_wavsave(const std::string& raw, int ch, int n, int sr, int bits, const std::string& out) {
+    std::vector<float> v = read_raw(raw, (size_t)ch * n);
+    if (v.empty() && ch * n) return 2;
+    std::vector<std::vector<float>> buf(ch, std::vector<float>(n));
+    for (int c = 0; c < ch; ++c)
+        for (int i = 0; i < n; ++i) buf[c][i] = v[(size_t)c * n + i];
+    AudioFile<float> f;
+    f.setAudioBuffer(buf);
+    f.setSampleRate(sr);
+    f.setBitDepth(bits);
+    return f.save(out) ? 0 : 3;
+}
+
+// the IR / output text dumps: std::ofstream << float << std::endl (AudioRenderer.cpp:552-556)
+int cmd_lines(const std::string& raw, int n, const std::string& out) {
+    std::vector<float> v = read_raw(raw, (size_t)n);
+    std::ofstream o(out);
+    for (int i = 0; i < n; ++i) o << v[i] << std::endl;
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -247,6 +277,10 @@ int main(int argc, char** argv) {
     if (cmd == "obj") return cmd_obj(argv[2]);
     if (cmd == "wav") return cmd_wav(argv[2]);
     if (cmd == "config") return cmd_config(argv[2]);
+    if (cmd == "wavsave" && argc >= 8)
+        return cmd_wavsave(argv[2], std::stoi(argv[3]), std::stoi(argv[4]), std::stoi(argv[5]), std::stoi(argv[6]),
+                           argv[7]);
+    if (cmd == "lines" && argc >= 5) return cmd_lines(argv[2], std::stoi(argv[3]), argv[4]);
     if (cmd == "receiver" && argc >= 8)
         return cmd_receiver(argv[2], argv[3], std::stof(argv[4]), std::stof(argv[5]), std::stof(argv[6]),
                             std::stof(argv[7]));

@@ -39,6 +39,17 @@ def test_live_block_matches_oracle(n_in):
         assert rel_err(got, ref) < 1e-12
 
 
+def test_prepared_spectra_follow_new_ir():
+    r, (irl, irr) = live_renderer(seed=3)
+    x = np.random.default_rng(4).uniform(-1, 1, 4096)
+    r.prepare_ir_spectra(file=True, live=True)
+    assert rel_err(r.convoluteLiveInput(x), po.convolute_live_block(x, irl, irr)) < 1e-12
+    irl2, irr2 = irr * 0.5, irl * 2.0  # new IR -> spectra must be recomputed
+    r.set_ir(irl2, irr2)
+    r.prepare_ir_spectra(file=True, live=True)
+    assert rel_err(r.convoluteLiveInput(x), po.convolute_live_block(x, irl2, irr2)) < 1e-12
+
+
 def test_live_block_48k_and_oversize():
     r, (irl, irr) = live_renderer(sr=48000)
     x = np.random.default_rng(1).uniform(-1, 1, 4096)
