@@ -227,6 +227,176 @@ void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset) {
     fix(b.root.ref, b.root.count);
 }
 
+namespace {
+
+ChildRef child_of(const BvhNode& n, int c) {
+    ChildRef r;
+    const float* ab = c == 0 ? n.a : n.b;
+    r.lo[0] = ab[0];
+    r.hi[0] = ab[1];
+    r.lo[1] = ab[2];
+    r.hi[1] = ab[3];
+    r.lo[2] = n.c[2 * c];
+    r.hi[2] = n.c[2 * c + 1];
+    r.ref = n.d[c];
+    r.count = n.d[2 + c];
+    return r;
+}
+
+float child_area(const ChildRef& c) {
+    const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+template <int W>
+void set_slot(WideNode<W>& n, int s, const ChildRef& c) {
+    n.lox[s] = c.lo[0];
+    n.hix[s] = c.hi[0];
+    n.loy[s] = c.lo[1];
+    n.hiy[s] = c.hi[1];
+    n.loz[s] = c.lo[2];
+    n.hiz[s] = c.hi[2];
+    n.ref[s] = c.ref;
+    n.cnt[s] = c.count;
+}
+
+template <int W>
+WideNode<W> empty_wide() {
+    WideNode<W> n;
+    const ChildRef e = empty_child();
+    for (int s = 0; s < W; ++s) set_slot(n, s, e);
+    return n;
+}
+
+template <int W>
+struct Collapser {
+    const BvhBuild* b;
+    int32_t bin_offset;
+    std::vector<WideNode<W>> nodes;
+    int depth = 0;
+
+    void expand(const ChildRef& inner, std::vector<ChildRef>& kids) const {
+        const BvhNode& n = b->nodes[(size_t)(inner.ref - bin_offset)];
+        for (int c = 0; c < 2; ++c) {
+            ChildRef k = child_of(n, c);
+            if (k.count >= 0) kids.push_back(k);
+        }
+    }
+
+    int32_t emit(const ChildRef& inner, int level) {
+        depth = std::max(depth, level);
+        std::vector<ChildRef> kids;
+        expand(inner, kids);
+        while ((int)kids.size() < W) {
+            int best = -1;
+            float best_area = -1.0f;
+            for (size_t i = 0; i < kids.size(); ++i) {
+                if (kids[i].count != 0) continue;
+                const float a = child_area(kids[i]);
+                if (a > best_area) {
+                    best_area = a;
+                    best = (int)i;
+                }
+            }
+            if (best < 0) break;
+            const ChildRef k = kids[(size_t)best];
+            kids.erase(kids.begin() + best);
+            expand(k, kids);
+        }
+        const int32_t me = (int32_t)nodes.size();
+        nodes.push_back(empty_wide<W>());
+        WideNode<W> n = empty_wide<W>();
+        for (size_t i = 0; i < kids.size(); ++i) {
+            ChildRef c = kids[i];
+            if (c.count == 0) c.ref = emit(c, level + 1);
+            set_slot(n, (int)i, c);
+        }
+        nodes[(size_t)me] = n;
+        return me;
+    }
+};
+
+template <int W>
+void collapse_impl(const BvhBuild& b, int32_t bin_offset, int32_t wide_offset, WideBuild& out) {
+    Collapser<W> c;
+    c.b = &b;
+    c.bin_offset = bin_offset;
+    out.root = b.root;
+    out.depth = 0;
+    if (b.root.count == 0) {
+        out.root.ref = c.emit(b.root, 1);
+        out.depth = c.depth;
+    }
+    // relocate inner references to their final position
+    for (WideNode<W>& n : c.nodes)
+        for (int s = 0; s < W; ++s)
+            if (n.cnt[s] == 0) n.ref[s] += wide_offset;
+    if (out.root.count == 0) out.root.ref += wide_offset;
+    out.width = W;
+    out.count = c.nodes.size();
+    out.bytes.resize(out.count * sizeof(WideNode<W>));
+    if (out.count) std::memcpy(out.bytes.data(), c.nodes.data(), out.bytes.size());
+}
+
+template <int W>
+bool validate_wide_impl(const WideNode<W>* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                        const char** why) {
+    for (size_t k = 0; k < n_nodes; ++k) {
+        const size_t i = first + k;
+        for (int s = 0; s < W; ++s) {
+            const int32_t ref = nodes[k].ref[s], count = nodes[k].cnt[s];
+            if (count < 0) continue;
+            if (count > 0) {
+                if (ref < 0 || (size_t)ref + (size_t)count > n_tris) {
+                    *why = "wide leaf range out of bounds";
+                    return false;
+                }
+                if (count > 15 || ref >= (1 << 27)) {
+                    *why = "wide leaf larger than 15 triangles or beyond 2^27";
+                    return false;
+                }
+            } else if (ref <= (int64_t)i || (size_t)ref >= total_nodes) {
+                *why = "wide inner child index not after its parent";
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+}  // namespace
+
+size_t wide_node_bytes(int width) { return width == 8 ? sizeof(WideNode<8>) : sizeof(WideNode<4>); }
+
+void collapse_bvh(const BvhBuild& b, int32_t bin_offset, int width, int32_t wide_offset, WideBuild& out) {
+    if (width == 8)
+        collapse_impl<8>(b, bin_offset, wide_offset, out);
+    else
+        collapse_impl<4>(b, bin_offset, wide_offset, out);
+}
+
+void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<uint8_t>& out) {
+    out.resize(wide_node_bytes(width));
+    if (width == 8) {
+        WideNode<8> n = empty_wide<8>();
+        set_slot(n, 0, a);
+        set_slot(n, 1, b);
+        std::memcpy(out.data(), &n, sizeof(n));
+    } else {
+        WideNode<4> n = empty_wide<4>();
+        set_slot(n, 0, a);
+        set_slot(n, 1, b);
+        std::memcpy(out.data(), &n, sizeof(n));
+    }
+}
+
+bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                   const char** why) {
+    if (width == 8)
+        return validate_wide_impl(reinterpret_cast<const WideNode<8>*>(nodes), first, n_nodes, total_nodes, n_tris, why);
+    return validate_wide_impl(reinterpret_cast<const WideNode<4>*>(nodes), first, n_nodes, total_nodes, n_tris, why);
+}
+
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why) {
     // Every inner child must have a larger index than its parent (the builder emits nodes in
     // pre-order): that makes the graph acyclic, so traversal always terminates.

@@ -32,4 +32,24 @@ ChildRef empty_child();
 // Structural check of a device-ready node array (acyclic, references in range).
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why);
 
+// Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
+struct WideBuild {
+    int width = 0;
+    std::vector<uint8_t> bytes;  // n * sizeof(WideNode<W>)
+    size_t count = 0;
+    ChildRef root;               // inner: wide node index (after relocation)
+    int depth = 0;               // wide levels on the longest root path
+};
+size_t wide_node_bytes(int width);
+// Collapse `b` (its inner refs offset by bin_offset) into W-wide nodes numbered from
+// wide_offset; leaf triangle ranges are shared with the binary layout.  Each wide node takes
+// the binary children of largest surface area first (Wald et al. 2008 style collapse).
+void collapse_bvh(const BvhBuild& b, int32_t bin_offset, int width, int32_t wide_offset, WideBuild& out);
+// Wide top node: slot 0 = scene root, slot 1 = receiver root.
+void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<uint8_t>& out);
+// Checks nodes [first, first + n_nodes) of a wide array of total_nodes nodes (`nodes` points
+// at node `first`): inner children after their parent and in range, leaf ranges in range.
+bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                   const char** why);
+
 }  // namespace arx

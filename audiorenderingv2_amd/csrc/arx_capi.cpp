@@ -77,6 +77,14 @@ struct arx_renderer {
     size_t nodes_cap = 0;
     TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
+    // wide tree for trace_width() > 2 (collapsed from the binary builds above)
+    int wide_w = 0;
+    WideBuild scene_w, recv_w;
+    uint8_t* d_wnodes = nullptr;
+    size_t wnodes_cap = 0;  // bytes
+    int32_t* d_spill = nullptr;
+    size_t spill_cap = 0;   // int32 entries
+    int32_t stack_need = 0;
     unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
     unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
     unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
@@ -153,8 +161,62 @@ void place_vertices(const float* local, int64_t n_vertices, float x, float y, fl
     }
 }
 
+// Wide-tree image of the current scene + receiver: [top | scene | receiver] WideNode<W>s,
+// re-collapsed only for the parts that changed; the spill stack is sized for the tree.
+arx_status ensure_wide(arx_renderer* r, bool scene_changed, bool recv_changed) {
+    const int W = trace_width();
+    if (W <= 2) return ARX_OK;
+    const size_t nb = wide_node_bytes(W);
+    bool scene_new = scene_changed || r->wide_w != W;
+    if (scene_new) collapse_bvh(r->scene, 1, W, 1, r->scene_w);
+    const bool recv_new = scene_new || recv_changed;
+    if (recv_new)
+        collapse_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), W, 1 + (int32_t)r->scene_w.count, r->recv_w);
+    r->wide_w = W;
+    const size_t total = 1 + r->scene_w.count + r->recv_w.count;
+    const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
+    if (total * nb > r->wnodes_cap) {
+        if (r->d_wnodes) ARX_HIP(hipFree(r->d_wnodes));
+        r->d_wnodes = nullptr;
+        const size_t cap = (total + 256) * nb;
+        ARX_HIP(hipMalloc(&r->d_wnodes, cap));
+        r->wnodes_cap = cap;
+        scene_new = true;
+    }
+    if (!(scene_new || recv_new)) return ARX_OK;
+    const char* why = "";
+    if (scene_new && !validate_wide(W, r->scene_w.bytes.data(), 1, r->scene_w.count, total, n_tris, &why))
+        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (scene): %s", why);
+    if (!validate_wide(W, r->recv_w.bytes.data(), 1 + r->scene_w.count, r->recv_w.count, total, n_tris, &why))
+        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (receiver): %s", why);
+    std::vector<uint8_t> top;
+    make_wide_top(W, r->scene_w.root, r->recv_w.root, top);
+    if (!validate_wide(W, top.data(), 0, 1, total, n_tris, &why))
+        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (top): %s", why);
+    ARX_HIP(hipMemcpyAsync(r->d_wnodes, top.data(), nb, hipMemcpyHostToDevice, r->stream));
+    if (scene_new && r->scene_w.count)
+        ARX_HIP(hipMemcpyAsync(r->d_wnodes + nb, r->scene_w.bytes.data(), r->scene_w.bytes.size(),
+                               hipMemcpyHostToDevice, r->stream));
+    if (r->recv_w.count)
+        ARX_HIP(hipMemcpyAsync(r->d_wnodes + (1 + r->scene_w.count) * nb, r->recv_w.bytes.data(),
+                               r->recv_w.bytes.size(), hipMemcpyHostToDevice, r->stream));
+    // worst-case stack: every level of the deepest path leaves W-1 siblings behind
+    const int depth = 1 + std::max(r->scene_w.depth, r->recv_w.depth);
+    r->stack_need = (W - 1) * depth + 2;
+    const size_t need = (size_t)r->stack_need * trace_spill_lanes(r->cus);
+    if (need > r->spill_cap) {
+        if (r->d_spill) ARX_HIP(hipFree(r->d_spill));
+        r->d_spill = nullptr;
+        ARX_HIP(hipMalloc(&r->d_spill, need * sizeof(int32_t)));
+        r->spill_cap = need;
+    }
+    ARX_HIP(hipStreamSynchronize(r->stream));  // pageable host sources
+    return ARX_OK;
+}
+
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_set) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
+    const bool scene_changed = r->scene_dirty, recv_changed = r->recv_dirty;
     if (r->recv_dirty) {
         // receiver halves placed in world space, left then right (placeReceiver OptixModel.cpp:153-157)
         std::vector<float> tv;
@@ -217,6 +279,8 @@ arx_status ensure_device_scene(arx_renderer* r) {
         // the host vectors are pageable: make sure the copies are done before they can change
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
+    arx_status st = ensure_wide(r, scene_changed || full, recv_changed);
+    if (st != ARX_OK) return st;
     r->scene_dirty = false;
     r->recv_dirty = false;
     r->stats.n_scene_tris = r->n_scene;
@@ -327,6 +391,8 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_live_out);
     hipFree(r->d_nodes);
     hipFree(r->d_tris);
+    hipFree(r->d_wnodes);
+    hipFree(r->d_spill);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
@@ -475,6 +541,10 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.is_mono = c.is_mono;
     a.max_visits = (int32_t)std::min<size_t>(r->nodes_cap + 8, 0x7fffffff);
     a.bvh_depth = r->stats.bvh_depth;
+    a.wnodes = r->d_wnodes;
+    a.spill = r->d_spill;
+    a.spill_lanes = trace_spill_lanes(r->cus);
+    a.stack_need = r->stack_need;
     if (ray_end == ray_begin) return ARX_OK;
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream));

@@ -14,6 +14,10 @@ int trace_grid_size(uint64_t n_rays, int device_cus);
 // cus = compute units of the device (grid sizing); the variant comes from ARX_TRACE_KERNEL.
 hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s);
 int trace_variant();
+// Node width the current variant traverses: 2 (BvhNode) or 4 / 8 (WideNode<W>, a.wnodes).
+int trace_width();
+// Upper bound on the lanes a persistent wide-tree launch uses (spill buffer columns).
+inline uint64_t trace_spill_lanes(int cus) { return (uint64_t)(cus > 0 ? cus : 256) * 2048ull; }
 // i64 histogram -> f32 IR (+ mono merge); unit = e0 * 2^-frac_bits.
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len,
                               double unit, int32_t is_mono, hipStream_t s);

@@ -37,6 +37,18 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
+// Wide node (W = 4: 128 B = one L2 line; W = 8: 256 B), collapsed from the binary SAH tree.
+// Boxes are stored per axis and bound (SoA) so one 16-B load brings the same plane of four
+// children; ref/cnt as in BvhNode (cnt 0 inner, > 0 leaf, -1 empty slot).
+template <int W>
+struct alignas(16) WideNode {
+    float lox[W], hix[W], loy[W], hiy[W], loz[W], hiz[W];
+    int32_t ref[W];
+    int32_t cnt[W];
+};
+static_assert(sizeof(WideNode<4>) == 128, "WideNode<4> must be 128 B");
+static_assert(sizeof(WideNode<8>) == 256, "WideNode<8> must be 256 B");
+
 // LDS traversal stack depth per lane; the builder caps tree depth below it.
 constexpr int kStackDepth = 40;      // v1/v2 (A/B variants): trees up to depth 39
 constexpr int kMaxStackDepth = 64;   // deepest stack variant of the default kernel
@@ -66,6 +78,12 @@ struct TraceArgs {
     int32_t is_mono;
     int32_t max_visits;  // traversal guard: > number of inner nodes (each is visited at most once)
     int32_t bvh_depth;   // inner levels on the longest root path (top node included) = max stack use
+    // wide-tree kernels (trace_width() > 2)
+    const void* wnodes;  // WideNode<W>[], node 0 = top (scene root, receiver root)
+    int32_t* spill;      // traversal-stack overflow beyond the LDS part: [depth][spill_lanes]
+    uint64_t spill_lanes;
+    int32_t stack_need;  // worst-case stack entries for this tree: (W-1) * wide depth + 2
+    int32_t spill_depth; // set by the launcher: stack_need - LDS entries (>= 0)
 };
 
 }  // namespace arx

@@ -691,6 +691,236 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
 }
 
+// ---------------------------------------------------------------- wide tree (v4) ---
+// Same persistent-wave scheme as v3 over W-wide nodes (W = 4: one 128-B line per node):
+// the dependent node-fetch chain per query is about half (W=4) or a third (W=8) of BVH2's.
+// Per node step all W child boxes are tested (their planes arrive as SoA float4s), the hit
+// children are sorted by entry distance with a sorting network, the nearest inner child is
+// visited next, the nearest leaf is parked as the pending leaf, and the rest are pushed far
+// to near.  The stack keeps S entries per lane in LDS and spills deeper entries to a
+// per-lane global region sized on the host for the tree's worst case.
+template <int BLOCK, int S>
+__device__ __forceinline__ void pushw(const TraceArgs& a, Trav3& t, int* __restrict__ stk, int lane, uint32_t gid, int v,
+                                      bool& overflow) {
+    if (t.sp < S) {
+        stk[t.sp * BLOCK + lane] = v;
+    } else if (t.sp - S < a.spill_depth) {
+        a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid] = v;
+    } else {
+        overflow = true;
+        return;
+    }
+    ++t.sp;
+}
+
+template <int BLOCK, int S>
+__device__ __forceinline__ int popw(const TraceArgs& a, Trav3& t, const int* __restrict__ stk, int lane, uint32_t gid) {
+    --t.sp;
+    if (t.sp < S) return stk[t.sp * BLOCK + lane];
+    return a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid];
+}
+
+__device__ __forceinline__ void cswap(float& ka, int& va, float& kb, int& vb) {
+    const bool sw = kb < ka;
+    const float k = sw ? kb : ka;
+    const int v = sw ? vb : va;
+    kb = sw ? ka : kb;
+    vb = sw ? va : vb;
+    ka = k;
+    va = v;
+}
+
+template <int W>
+__device__ __forceinline__ void sort_children(float* k, int* v) {
+    if constexpr (W == 4) {
+        cswap(k[0], v[0], k[1], v[1]);
+        cswap(k[2], v[2], k[3], v[3]);
+        cswap(k[0], v[0], k[2], v[2]);
+        cswap(k[1], v[1], k[3], v[3]);
+        cswap(k[1], v[1], k[2], v[2]);
+    } else {  // Batcher's 8-input network, 19 comparators
+        cswap(k[0], v[0], k[1], v[1]); cswap(k[2], v[2], k[3], v[3]);
+        cswap(k[4], v[4], k[5], v[5]); cswap(k[6], v[6], k[7], v[7]);
+        cswap(k[0], v[0], k[2], v[2]); cswap(k[1], v[1], k[3], v[3]);
+        cswap(k[4], v[4], k[6], v[6]); cswap(k[5], v[5], k[7], v[7]);
+        cswap(k[1], v[1], k[2], v[2]); cswap(k[5], v[5], k[6], v[6]);
+        cswap(k[0], v[0], k[4], v[4]); cswap(k[1], v[1], k[5], v[5]);
+        cswap(k[2], v[2], k[6], v[6]); cswap(k[3], v[3], k[7], v[7]);
+        cswap(k[2], v[2], k[4], v[4]); cswap(k[3], v[3], k[5], v[5]);
+        cswap(k[1], v[1], k[2], v[2]); cswap(k[3], v[3], k[4], v[4]);
+        cswap(k[5], v[5], k[6], v[6]);
+    }
+}
+
+template <int W, int BLOCK, int S>
+__device__ __forceinline__ void node_step_w(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                            int* __restrict__ stk, int lane, uint32_t gid, bool& overflow) {
+    if (t.node < 0) {  // pop
+        const int e = popw<BLOCK, S>(a, t, stk, lane, gid);
+        if (e >= 0) {
+            t.node = e;
+        } else {
+            const int v = -e - 1;
+            t.pf = v >> 4;
+            t.pc = v & 15;
+            return;
+        }
+    }
+    if (++t.visits > a.max_visits) {  // malformed tree guard: end the query, flag the launch
+        overflow = true;
+        t.node = -1;
+        t.sp = 0;
+        return;
+    }
+    const float4* np = reinterpret_cast<const float4*>(reinterpret_cast<const WideNode<W>*>(a.wnodes) + t.node);
+    constexpr int Q = W / 4;  // float4s per plane array
+    float lx[W], hx[W], ly[W], hy[W], lz[W], hz[W];
+    int ref[W], cnt[W];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float4 v0 = np[0 * Q + q], v1 = np[1 * Q + q], v2 = np[2 * Q + q];
+        const float4 v3 = np[3 * Q + q], v4 = np[4 * Q + q], v5 = np[5 * Q + q];
+        const int4 v6 = *reinterpret_cast<const int4*>(np + 6 * Q + q);
+        const int4 v7 = *reinterpret_cast<const int4*>(np + 7 * Q + q);
+        lx[4 * q + 0] = v0.x; lx[4 * q + 1] = v0.y; lx[4 * q + 2] = v0.z; lx[4 * q + 3] = v0.w;
+        hx[4 * q + 0] = v1.x; hx[4 * q + 1] = v1.y; hx[4 * q + 2] = v1.z; hx[4 * q + 3] = v1.w;
+        ly[4 * q + 0] = v2.x; ly[4 * q + 1] = v2.y; ly[4 * q + 2] = v2.z; ly[4 * q + 3] = v2.w;
+        hy[4 * q + 0] = v3.x; hy[4 * q + 1] = v3.y; hy[4 * q + 2] = v3.z; hy[4 * q + 3] = v3.w;
+        lz[4 * q + 0] = v4.x; lz[4 * q + 1] = v4.y; lz[4 * q + 2] = v4.z; lz[4 * q + 3] = v4.w;
+        hz[4 * q + 0] = v5.x; hz[4 * q + 1] = v5.y; hz[4 * q + 2] = v5.z; hz[4 * q + 3] = v5.w;
+        ref[4 * q + 0] = v6.x; ref[4 * q + 1] = v6.y; ref[4 * q + 2] = v6.z; ref[4 * q + 3] = v6.w;
+        cnt[4 * q + 0] = v7.x; cnt[4 * q + 1] = v7.y; cnt[4 * q + 2] = v7.z; cnt[4 * q + 3] = v7.w;
+    }
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float inf = __builtin_huge_valf();
+    float key[W];
+    int code[W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+        const float x0 = __builtin_fmaf(lx[c], ix, -oix), x1 = __builtin_fmaf(hx[c], ix, -oix);
+        const float y0 = __builtin_fmaf(ly[c], iy, -oiy), y1 = __builtin_fmaf(hy[c], iy, -oiy);
+        const float z0 = __builtin_fmaf(lz[c], iz, -oiz), z1 = __builtin_fmaf(hz[c], iz, -oiz);
+        const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t.best_t));
+        const bool hit = tn <= tf && cnt[c] >= 0;
+        key[c] = hit ? tn : inf;
+        code[c] = cnt[c] > 0 ? leaf_code(ref[c], cnt[c]) : ref[c];
+    }
+    sort_children<W>(key, code);
+    // nearest inner child -> next node, nearest leaf -> pending; the rest pushed far to near
+    int next = -1, leaf = 0;
+    bool got_inner = false, got_leaf = false;
+    bool skip[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        const bool h = key[j] < inf;
+        const bool take_inner = h && code[j] >= 0 && !got_inner;
+        const bool take_leaf = h && code[j] < 0 && !got_leaf;
+        next = take_inner ? code[j] : next;
+        leaf = take_leaf ? code[j] : leaf;
+        got_inner = got_inner || take_inner;
+        got_leaf = got_leaf || take_leaf;
+        skip[j] = !h || take_inner || take_leaf;
+    }
+#pragma unroll
+    for (int j = W - 1; j >= 0; --j)
+        if (!skip[j]) pushw<BLOCK, S>(a, t, stk, lane, gid, code[j], overflow);
+    t.node = next;
+    if (got_leaf) {
+        const int v = -leaf - 1;
+        t.pf = v >> 4;
+        t.pc = v & 15;
+    }
+}
+
+template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_w(TraceArgs a) {
+    __shared__ int stk[S * BLOCK];
+    const int lane = threadIdx.x;
+    const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    unsigned long long* const cursor = a.counters + 4;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    bool overflow = false;
+    bool active = false;
+    bool trav = false;
+    bool exhausted = false;
+    RayState s;
+    Ray r;
+    Trav3 t;
+    float oix = 0.f, oiy = 0.f, oiz = 0.f;
+    s.depth = -1;
+    t.best_t = __builtin_huge_valf();
+    t.best_id = 0x7fffffff;
+    t.best = -1;
+    t.node = -1;
+    t.sp = 0;
+    t.pf = 0;
+    t.pc = 0;
+    t.visits = 0;
+    while (true) {
+        if (active && !trav) {
+            shade(a, s, r, t.best, n_rx, n_miss);
+            if (!wants_query(a, s)) active = false;
+        }
+        const unsigned long long need = __ballot(!active);
+        if (need != 0ull && !exhausted) {
+            const int cnt = __popcll(need);
+            const int leader = __ffsll((unsigned long long)need) - 1;
+            unsigned long long base = 0;
+            if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+            base = ((unsigned long long)hi << 32) | lo;
+            if (!active) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint64_t i = base + rank;
+                if (i < n) {
+                    ray_init(a, s, a.ray_begin + i);
+                    active = wants_query(a, s);
+                }
+            }
+            if (base + (unsigned long long)cnt >= n) exhausted = true;
+        }
+        if (active && !trav) {
+            ++n_q;
+            setup_ray(r, s.pos, s.dir);
+            oix = r.o[0] * r.inv[0];
+            oiy = r.o[1] * r.inv[1];
+            oiz = r.o[2] * r.inv[2];
+            t.best_t = __builtin_huge_valf();
+            t.best_id = 0x7fffffff;
+            t.best = -1;
+            t.node = 0;
+            t.sp = 0;
+            t.pc = 0;
+            t.pf = 0;
+            t.visits = 0;
+            trav = true;
+        }
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        while (true) {
+            if (trav && t.pc == 0 && t.node < 0 && t.sp == 0) trav = false;  // query finished
+            const bool can_node = trav && t.pc == 0;
+            const unsigned long long m_node = __ballot(can_node);
+            const unsigned long long m_leaf = __ballot(trav && t.pc > 0);
+            if ((m_node | m_leaf) == 0ull) break;
+            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+                if (can_node) node_step_w<W, BLOCK, S>(a, r, oix, oiy, oiz, t, stk, lane, gid, overflow);
+            } else if (trav && t.pc > 0) {
+                leaf_hits(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
+                t.pc = 0;
+            }
+        }
+    }
+    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+}
+
 __global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __restrict__ L, float* __restrict__ R,
                                    int32_t ir_len, double unit, int32_t mono) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -751,7 +981,31 @@ hipError_t launch_v3(const TraceArgs& a, int cus, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
+template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW>
+hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
+    if (!a.wnodes) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
+    if (e != hipSuccess) return e;
+    auto k = trace_kernel_w<W, BLOCK, S, THRESH, LEAF_THRESH, MINW>;
+    int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
+    a.spill_depth = a.stack_need > S ? a.stack_need - S : 0;
+    if (a.spill_depth > 0) {
+        if (!a.spill) return hipErrorInvalidValue;
+        const uint64_t max_grid = a.spill_lanes / BLOCK;  // every lane owns a spill column
+        if ((uint64_t)grid > max_grid) grid = (int)max_grid;
+        if (grid <= 0) return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
 }  // namespace
+
+int trace_width() {
+    const int v = trace_variant();
+    if (v >= 300 && v < 310) return 4;
+    if (v >= 310 && v < 320) return 8;
+    return 2;
+}
 
 int trace_variant() {
     const char* v = getenv("ARX_TRACE_KERNEL");
@@ -807,6 +1061,19 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 206: return launch_v3<128, 28, 12, 32, 5>(a, cus, s);
         case 207: return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
         case 2: return launch_v2<128, 16>(a, cus, s);
+        // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
+        case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
+        case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
+        case 302: return launch_w<4, 128, 16, 32, 12, 6>(a, cus, s);
+        case 303: return launch_w<4, 64, 24, 16, 12, 5>(a, cus, s);
+        case 304: return launch_w<4, 128, 24, 16, 12, 5>(a, cus, s);
+        case 305: return launch_w<4, 128, 24, 48, 12, 5>(a, cus, s);
+        case 306: return launch_w<4, 128, 24, 32, 24, 5>(a, cus, s);
+        case 307: return launch_w<4, 128, 20, 32, 12, 4>(a, cus, s);
+        case 310: return launch_w<8, 128, 24, 32, 12, 4>(a, cus, s);
+        case 311: return launch_w<8, 128, 32, 32, 12, 4>(a, cus, s);
+        case 312: return launch_w<8, 128, 16, 32, 12, 5>(a, cus, s);
+        case 313: return launch_w<8, 64, 24, 16, 12, 4>(a, cus, s);
         default:
             if (a.bvh_depth < 28) return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
             if (a.bvh_depth < 40) return launch_v3<128, 32, 12, 40, 5>(a, cus, s);

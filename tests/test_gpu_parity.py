@@ -155,10 +155,31 @@ def test_full_size_c3_properties(conference):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "143", "207"])
+@pytest.mark.parametrize("variant", ["300", "307", "310", "312"])
+def test_wide_tree_variants_match_oracle(c1_scene, conference, monkeypatch, variant):
+    """4- and 8-wide trees (incl. LDS-stack spill variants) against the oracle: C1 dense,
+    a listener move (receiver-only re-collapse) and an empty scene."""
+    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
+    s = RenderSettings(rays=(64, 64, 8), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
+    em = (0.5, 3.0, 1.0)
+    r = make(c1_scene, (2.5, 9.9, 0.0), emitter=em, **s.__dict__)
+    assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em, s)
+    s = RenderSettings(rays=(40, 40, 10), sample_rate=16000, base_power=3.62, max_bounces=8)
+    r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    assert_same_render(r, conference, CONFERENCE_LISTENER, 0.0, CONFERENCE_EMITTER, s)
+    lst = (2.0, 1.4, -1.5)
+    r.setSphereCenterInOptix(lst, 33.0)
+    assert_same_render(r, conference, lst, 33.0, CONFERENCE_EMITTER, s)
+    empty = Scene(np.zeros((0, 9), np.float32), np.zeros(0, np.float32), [])
+    r = make(empty, (0.0, 0.0, 3.0), **s.__dict__)
+    gl, _, st = assert_same_render(r, empty, (0.0, 0.0, 3.0), 0.0, (0.0, 0.0, 0.0), s)
+    assert st["receiver_hits"] > 0
+
+
+@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312"])
 def test_kernel_variants_identical(conference, monkeypatch, variant):
     """Every trace-kernel variant (grid-stride v1, persistent v2, postponed-leaf v3 and its
-    tunings) produces the default kernel's histogram bit for bit."""
+    tunings, 4-/8-wide trees) produces the default kernel's histogram bit for bit."""
     s = RenderSettings(rays=(100, 100, 10), sample_rate=48000, base_power=3.62, max_bounces=16, hrtf_absorption_rate=0.5)
     r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
     monkeypatch.delenv("ARX_TRACE_KERNEL", raising=False)
