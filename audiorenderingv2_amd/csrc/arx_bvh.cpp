@@ -364,20 +364,125 @@ bool validate_wide_impl(const WideNode<W>* nodes, size_t first, size_t n_nodes, 
     return true;
 }
 
+// WideNode<4> -> QNode4: per axis, origin = node lo and the smallest power-of-two step with
+// 255 steps covering the node; child planes rounded outward (floor / ceil) in exact double
+// arithmetic, so every quantized box contains the child's padded box.
+QNode4 quantize4(const WideNode<4>& n) {
+    QNode4 q;
+    std::memset(&q, 0, sizeof(q));
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    bool any = false;
+    for (int s = 0; s < 4; ++s) {
+        if (n.cnt[s] < 0) continue;
+        any = true;
+        const float cl[3] = {n.lox[s], n.loy[s], n.loz[s]}, ch[3] = {n.hix[s], n.hiy[s], n.hiz[s]};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], (double)cl[k]);
+            hi[k] = std::max(hi[k], (double)ch[k]);
+        }
+    }
+    int e[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k) {
+        if (!any) {
+            lo[k] = hi[k] = 0.0;
+        }
+        q.origin[k] = (float)lo[k];  // a child's float coordinate: exact
+        const double ext = hi[k] - lo[k];
+        int ek = ext > 0.0 ? std::max(-100, (int)std::ceil(std::log2(ext / 255.0)) - 1) : -100;
+        while (std::ldexp(255.0, ek) < ext) ++ek;
+        e[k] = std::min(ek, 120);
+    }
+    q.exps = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
+    q.counts = 0;
+    for (int s = 0; s < 4; ++s) {
+        uint32_t cnt_byte = 0xFF;
+        if (n.cnt[s] >= 0) {
+            cnt_byte = (uint32_t)n.cnt[s];
+            const float cl[3] = {n.lox[s], n.loy[s], n.loz[s]}, ch[3] = {n.hix[s], n.hiy[s], n.hiz[s]};
+            for (int k = 0; k < 3; ++k) {
+                const double step = std::ldexp(1.0, e[k]);
+                double ql = std::floor(((double)cl[k] - (double)q.origin[k]) / step);
+                double qh = std::ceil(((double)ch[k] - (double)q.origin[k]) / step);
+                ql = std::max(0.0, std::min(255.0, ql));
+                qh = std::max(0.0, std::min(255.0, qh));
+                q.q[2 * k] |= (uint32_t)ql << (8 * s);
+                q.q[2 * k + 1] |= (uint32_t)qh << (8 * s);
+            }
+        }
+        q.counts |= cnt_byte << (8 * s);
+        q.ref[s] = n.cnt[s] >= 0 ? n.ref[s] : 0;
+    }
+    return q;
+}
+
+void to_q4(WideBuild& out) {
+    const WideNode<4>* w = reinterpret_cast<const WideNode<4>*>(out.bytes.data());
+    std::vector<uint8_t> bytes(out.count * sizeof(QNode4));
+    QNode4* q = reinterpret_cast<QNode4*>(bytes.data());
+    for (size_t i = 0; i < out.count; ++i) q[i] = quantize4(w[i]);
+    out.bytes.swap(bytes);
+    out.width = kWideQ4;
+}
+
+bool validate_q4(const QNode4* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                 const char** why) {
+    for (size_t k = 0; k < n_nodes; ++k) {
+        const size_t i = first + k;
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t c = (nodes[k].counts >> (8 * s)) & 0xFF;
+            const int32_t ref = nodes[k].ref[s];
+            if (c == 0xFF) continue;
+            if (c > 15) {
+                *why = "q4 leaf larger than 15 triangles";
+                return false;
+            }
+            if (c > 0) {
+                if (ref < 0 || (size_t)ref + c > n_tris || ref >= (1 << 27)) {
+                    *why = "q4 leaf range out of bounds";
+                    return false;
+                }
+            } else if (ref <= (int64_t)i || (size_t)ref >= total_nodes) {
+                *why = "q4 inner child index not after its parent";
+                return false;
+            }
+        }
+        const uint32_t ex = nodes[k].exps;
+        for (int a = 0; a < 3; ++a) {
+            const int be = (int)((ex >> (8 * a)) & 0xFF);
+            if (be < 1 || be > 254) {
+                *why = "q4 exponent out of range";
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
-size_t wide_node_bytes(int width) { return width == 8 ? sizeof(WideNode<8>) : sizeof(WideNode<4>); }
+size_t wide_node_bytes(int width) {
+    if (width == kWideQ4) return sizeof(QNode4);
+    return width == 8 ? sizeof(WideNode<8>) : sizeof(WideNode<4>);
+}
 
 void collapse_bvh(const BvhBuild& b, int32_t bin_offset, int width, int32_t wide_offset, WideBuild& out) {
-    if (width == 8)
+    if (width == 8) {
         collapse_impl<8>(b, bin_offset, wide_offset, out);
-    else
+    } else {
         collapse_impl<4>(b, bin_offset, wide_offset, out);
+        if (width == kWideQ4) to_q4(out);
+    }
 }
 
 void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<uint8_t>& out) {
     out.resize(wide_node_bytes(width));
-    if (width == 8) {
+    if (width == kWideQ4) {
+        WideNode<4> n = empty_wide<4>();
+        set_slot(n, 0, a);
+        set_slot(n, 1, b);
+        const QNode4 q = quantize4(n);
+        std::memcpy(out.data(), &q, sizeof(q));
+    } else if (width == 8) {
         WideNode<8> n = empty_wide<8>();
         set_slot(n, 0, a);
         set_slot(n, 1, b);
@@ -392,6 +497,8 @@ void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<
 
 bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
                    const char** why) {
+    if (width == kWideQ4)
+        return validate_q4(reinterpret_cast<const QNode4*>(nodes), first, n_nodes, total_nodes, n_tris, why);
     if (width == 8)
         return validate_wide_impl(reinterpret_cast<const WideNode<8>*>(nodes), first, n_nodes, total_nodes, n_tris, why);
     return validate_wide_impl(reinterpret_cast<const WideNode<4>*>(nodes), first, n_nodes, total_nodes, n_tris, why);

@@ -1,6 +1,7 @@
 // arx_bvh.hpp -- host-side SAH BVH builder (replaces optixAccelBuild/optixAccelCompact,
 // R/prebuild/obj_raytracer/AudioRenderer.cpp:179-208).
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 

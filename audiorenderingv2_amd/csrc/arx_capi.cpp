@@ -202,7 +202,8 @@ arx_status ensure_wide(arx_renderer* r, bool scene_changed, bool recv_changed) {
                                r->recv_w.bytes.size(), hipMemcpyHostToDevice, r->stream));
     // worst-case stack: every level of the deepest path leaves W-1 siblings behind
     const int depth = 1 + std::max(r->scene_w.depth, r->recv_w.depth);
-    r->stack_need = (W - 1) * depth + 2;
+    const int fanout = (W == kWideQ4) ? 4 : W;
+    r->stack_need = (fanout - 1) * depth + 2;
     const size_t need = (size_t)r->stack_need * trace_spill_lanes(r->cus);
     if (need > r->spill_cap) {
         if (r->d_spill) ARX_HIP(hipFree(r->d_spill));

@@ -49,6 +49,25 @@ struct alignas(16) WideNode {
 static_assert(sizeof(WideNode<4>) == 128, "WideNode<4> must be 128 B");
 static_assert(sizeof(WideNode<8>) == 256, "WideNode<8> must be 256 B");
 
+// Quantized 4-wide node, 64 B (4 x 16-B loads), child boxes on an 8-bit grid per axis:
+// plane = origin + q * 2^e (exact in real arithmetic), rounded outward when built so every
+// child box contains its padded exact box (conservative; Ylitie et al. 2017 style).
+//   dword 0-2 origin xyz (f32), dword 3 biased exponents ex | ey << 8 | ez << 16
+//   dword 4-9 qlo.x, qhi.x, qlo.y, qhi.y, qlo.z, qhi.z: byte c = child c
+//   dword 10 counts: byte c = 0 inner, 1..15 leaf, 0xFF empty;  dword 11 unused
+//   dword 12-15 ref[4]: inner node index / first triangle
+struct alignas(16) QNode4 {
+    float origin[3];
+    uint32_t exps;
+    uint32_t q[6];
+    uint32_t counts;
+    uint32_t pad;
+    int32_t ref[4];
+};
+static_assert(sizeof(QNode4) == 64, "QNode4 must be 64 B");
+// Node-format code of QNode4 trees where a "width" is passed (2, 4, 8 are BvhNode / WideNode<W>).
+constexpr int kWideQ4 = 5;
+
 // LDS traversal stack depth per lane; the builder caps tree depth below it.
 constexpr int kStackDepth = 40;      // v1/v2 (A/B variants): trees up to depth 39
 constexpr int kMaxStackDepth = 64;   // deepest stack variant of the default kernel

@@ -833,6 +833,84 @@ __device__ __forceinline__ void node_step_w(const TraceArgs& a, const Ray& r, fl
     }
 }
 
+__device__ __forceinline__ float ubyte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xFFu); }
+
+// QNode4 step: plane t = fma(q, 2^e * inv, fma(origin, inv, -o*inv)), i.e. the same slab
+// arithmetic as the f32 trees with the grid step folded into the reciprocal (2^e * inv is
+// exact); quantized boxes enclose the padded boxes, so culling stays conservative.
+template <int BLOCK, int S>
+__device__ __forceinline__ void node_step_q4(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz,
+                                             Trav3& t, int* __restrict__ stk, int lane, uint32_t gid, bool& overflow) {
+    if (t.node < 0) {  // pop
+        const int e = popw<BLOCK, S>(a, t, stk, lane, gid);
+        if (e >= 0) {
+            t.node = e;
+        } else {
+            const int v = -e - 1;
+            t.pf = v >> 4;
+            t.pc = v & 15;
+            return;
+        }
+    }
+    if (++t.visits > a.max_visits) {
+        overflow = true;
+        t.node = -1;
+        t.sp = 0;
+        return;
+    }
+    const uint4* np = reinterpret_cast<const uint4*>(reinterpret_cast<const QNode4*>(a.wnodes) + t.node);
+    const uint4 h0 = np[0], h1 = np[1], h2 = np[2];
+    const int4 rf = *reinterpret_cast<const int4*>(np + 3);
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float sx = __uint_as_float((h0.w & 0xFFu) << 23) * ix;
+    const float sy = __uint_as_float(((h0.w >> 8) & 0xFFu) << 23) * iy;
+    const float sz = __uint_as_float(((h0.w >> 16) & 0xFFu) << 23) * iz;
+    const float bx = __builtin_fmaf(__uint_as_float(h0.x), ix, -oix);
+    const float by = __builtin_fmaf(__uint_as_float(h0.y), iy, -oiy);
+    const float bz = __builtin_fmaf(__uint_as_float(h0.z), iz, -oiz);
+    const float inf = __builtin_huge_valf();
+    const int ref[4] = {rf.x, rf.y, rf.z, rf.w};
+    float key[4];
+    int code[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float x0 = __builtin_fmaf(ubyte(h1.x, c), sx, bx), x1 = __builtin_fmaf(ubyte(h1.y, c), sx, bx);
+        const float y0 = __builtin_fmaf(ubyte(h1.z, c), sy, by), y1 = __builtin_fmaf(ubyte(h1.w, c), sy, by);
+        const float z0 = __builtin_fmaf(ubyte(h2.x, c), sz, bz), z1 = __builtin_fmaf(ubyte(h2.y, c), sz, bz);
+        const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t.best_t));
+        const int cnt = (int)((h2.z >> (8 * c)) & 0xFFu);
+        const bool hit = tn <= tf && cnt != 0xFF;
+        key[c] = hit ? tn : inf;
+        code[c] = cnt > 0 ? leaf_code(ref[c], cnt) : ref[c];
+    }
+    sort_children<4>(key, code);
+    int next = -1, leaf = 0;
+    bool got_inner = false, got_leaf = false;
+    bool skip[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool h = key[j] < inf;
+        const bool take_inner = h && code[j] >= 0 && !got_inner;
+        const bool take_leaf = h && code[j] < 0 && !got_leaf;
+        next = take_inner ? code[j] : next;
+        leaf = take_leaf ? code[j] : leaf;
+        got_inner = got_inner || take_inner;
+        got_leaf = got_leaf || take_leaf;
+        skip[j] = !h || take_inner || take_leaf;
+    }
+#pragma unroll
+    for (int j = 3; j >= 0; --j)
+        if (!skip[j]) pushw<BLOCK, S>(a, t, stk, lane, gid, code[j], overflow);
+    t.node = next;
+    if (got_leaf) {
+        const int v = -leaf - 1;
+        t.pf = v >> 4;
+        t.pc = v & 15;
+    }
+}
+
+// W == kWideQ4 selects QNode4 trees
 template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_w(TraceArgs a) {
     __shared__ int stk[S * BLOCK];
@@ -911,7 +989,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_w(TraceArgs a) {
             if ((m_node | m_leaf) == 0ull) break;
             if (__popcll(__ballot(active && !trav)) >= THRESH) break;
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
-                if (can_node) node_step_w<W, BLOCK, S>(a, r, oix, oiy, oiz, t, stk, lane, gid, overflow);
+                if (can_node) {
+                    if constexpr (W == kWideQ4)
+                        node_step_q4<BLOCK, S>(a, r, oix, oiy, oiz, t, stk, lane, gid, overflow);
+                    else
+                        node_step_w<W, BLOCK, S>(a, r, oix, oiy, oiz, t, stk, lane, gid, overflow);
+                }
             } else if (trav && t.pc > 0) {
                 leaf_hits(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
                 t.pc = 0;
@@ -1004,6 +1087,7 @@ int trace_width() {
     const int v = trace_variant();
     if (v >= 300 && v < 310) return 4;
     if (v >= 310 && v < 320) return 8;
+    if (v >= 320 && v < 340) return kWideQ4;
     return 2;
 }
 
@@ -1074,6 +1158,17 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 311: return launch_w<8, 128, 32, 32, 12, 4>(a, cus, s);
         case 312: return launch_w<8, 128, 16, 32, 12, 5>(a, cus, s);
         case 313: return launch_w<8, 64, 24, 16, 12, 4>(a, cus, s);
+        // quantized 4-wide (QNode4, 64 B)
+        case 320: return launch_w<kWideQ4, 128, 24, 32, 12, 5>(a, cus, s);
+        case 321: return launch_w<kWideQ4, 128, 32, 32, 12, 5>(a, cus, s);
+        case 322: return launch_w<kWideQ4, 128, 16, 32, 12, 6>(a, cus, s);
+        case 323: return launch_w<kWideQ4, 128, 20, 32, 12, 4>(a, cus, s);
+        case 324: return launch_w<kWideQ4, 64, 24, 16, 12, 5>(a, cus, s);
+        case 325: return launch_w<kWideQ4, 128, 24, 16, 12, 5>(a, cus, s);
+        case 326: return launch_w<kWideQ4, 128, 24, 48, 12, 5>(a, cus, s);
+        case 327: return launch_w<kWideQ4, 128, 24, 32, 24, 5>(a, cus, s);
+        case 328: return launch_w<kWideQ4, 256, 24, 64, 12, 5>(a, cus, s);
+        case 329: return launch_w<kWideQ4, 128, 28, 32, 12, 5>(a, cus, s);
         default:
             if (a.bvh_depth < 28) return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
             if (a.bvh_depth < 40) return launch_v3<128, 32, 12, 40, 5>(a, cus, s);

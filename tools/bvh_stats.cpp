@@ -1,0 +1,247 @@
+// bvh_stats -- host-side traversal statistics of the trace kernel's trees (design tool).
+//
+// Builds the production binary SAH tree (arx_bvh.cpp) and its 4-/8-wide collapses, then
+// replays closest-hit queries of bouncing rays (specular reflection, same scene) and counts
+// per query: node visits, triangle tests and bytes fetched under each layout.  Used to pick
+// node formats: the trace kernel is bound by vector-memory instruction throughput.
+//
+//   g++ -O2 -std=c++17 -I audiorenderingv2_amd/csrc tools/bvh_stats.cpp \
+//       audiorenderingv2_amd/csrc/arx_bvh.cpp -o /tmp/bvh_stats
+//   /tmp/bvh_stats scene.f32 n_tris ex ey ez n_rays bounces
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "arx_bvh.hpp"
+
+using namespace arx;
+
+struct Q {
+    float o[3], d[3], inv[3];
+};
+
+static bool tri_hit(const TriRec& t, const Q& q, float& tt) {
+    // Moller-Trumbore (statistics only; the product uses the watertight test)
+    const float e1[3] = {t.v1[0] - t.v0[0], t.v1[1] - t.v0[1], t.v1[2] - t.v0[2]};
+    const float e2[3] = {t.v2[0] - t.v0[0], t.v2[1] - t.v0[1], t.v2[2] - t.v0[2]};
+    const float p[3] = {q.d[1] * e2[2] - q.d[2] * e2[1], q.d[2] * e2[0] - q.d[0] * e2[2], q.d[0] * e2[1] - q.d[1] * e2[0]};
+    const float det = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2];
+    if (std::fabs(det) < 1e-12f) return false;
+    const float inv = 1.0f / det;
+    const float s[3] = {q.o[0] - t.v0[0], q.o[1] - t.v0[1], q.o[2] - t.v0[2]};
+    const float u = (s[0] * p[0] + s[1] * p[1] + s[2] * p[2]) * inv;
+    if (u < 0 || u > 1) return false;
+    const float qq[3] = {s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0]};
+    const float v = (q.d[0] * qq[0] + q.d[1] * qq[1] + q.d[2] * qq[2]) * inv;
+    if (v < 0 || u + v > 1) return false;
+    tt = (e2[0] * qq[0] + e2[1] * qq[1] + e2[2] * qq[2]) * inv;
+    return tt >= 0;
+}
+
+static bool slab(const float lo[3], const float hi[3], const Q& q, float tmax, float& tn) {
+    float a = 0.0f, b = tmax;
+    for (int k = 0; k < 3; ++k) {
+        float t0 = (lo[k] - q.o[k]) * q.inv[k], t1 = (hi[k] - q.o[k]) * q.inv[k];
+        if (t0 > t1) std::swap(t0, t1);
+        a = std::max(a, t0);
+        b = std::min(b, t1);
+    }
+    tn = a;
+    return a <= b;
+}
+
+struct Stats {
+    double visits = 0, tests = 0, leaves = 0, maxstack = 0;
+};
+
+struct Tree {
+    int W;
+    std::vector<ChildRef> kids;  // W per node
+    size_t n = 0;
+};
+
+static Tree from_binary(const std::vector<BvhNode>& nodes, const BvhNode& top) {
+    Tree t;
+    t.W = 2;
+    t.n = nodes.size() + 1;
+    t.kids.resize(2 * t.n);
+    auto put = [&](size_t i, const BvhNode& n) {
+        for (int c = 0; c < 2; ++c) {
+            ChildRef& r = t.kids[2 * i + c];
+            const float* ab = c == 0 ? n.a : n.b;
+            r.lo[0] = ab[0]; r.hi[0] = ab[1]; r.lo[1] = ab[2]; r.hi[1] = ab[3];
+            r.lo[2] = n.c[2 * c]; r.hi[2] = n.c[2 * c + 1];
+            r.ref = n.d[c];
+            r.count = n.d[2 + c];
+        }
+    };
+    put(0, top);
+    for (size_t i = 0; i < nodes.size(); ++i) put(i + 1, nodes[i]);
+    return t;
+}
+
+template <int W>
+static Tree from_wide(const std::vector<uint8_t>& top, const WideBuild& w) {
+    Tree t;
+    t.W = W;
+    t.n = 1 + w.count;
+    t.kids.resize(W * t.n);
+    auto put = [&](size_t i, const WideNode<W>& n) {
+        for (int s = 0; s < W; ++s) {
+            ChildRef& r = t.kids[W * i + s];
+            r.lo[0] = n.lox[s]; r.hi[0] = n.hix[s]; r.lo[1] = n.loy[s]; r.hi[1] = n.hiy[s];
+            r.lo[2] = n.loz[s]; r.hi[2] = n.hiz[s];
+            r.ref = n.ref[s];
+            r.count = n.cnt[s];
+        }
+    };
+    put(0, *reinterpret_cast<const WideNode<W>*>(top.data()));
+    const WideNode<W>* p = reinterpret_cast<const WideNode<W>*>(w.bytes.data());
+    for (size_t i = 0; i < w.count; ++i) put(i + 1, p[i]);
+    return t;
+}
+
+static Tree from_q4(const std::vector<uint8_t>& top, const WideBuild& w) {
+    Tree t;
+    t.W = 4;
+    t.n = 1 + w.count;
+    t.kids.resize(4 * t.n);
+    auto put = [&](size_t i, const QNode4& n) {
+        for (int s = 0; s < 4; ++s) {
+            ChildRef& r = t.kids[4 * i + s];
+            const uint32_t c = (n.counts >> (8 * s)) & 0xFF;
+            r.count = c == 0xFF ? -1 : (int)c;
+            r.ref = n.ref[s];
+            for (int k = 0; k < 3; ++k) {
+                const int e = (int)((n.exps >> (8 * k)) & 0xFF) - 127;
+                const double step = std::ldexp(1.0, e);
+                r.lo[k] = (float)(n.origin[k] + ((n.q[2 * k] >> (8 * s)) & 0xFF) * step);
+                r.hi[k] = (float)(n.origin[k] + ((n.q[2 * k + 1] >> (8 * s)) & 0xFF) * step);
+            }
+        }
+    };
+    put(0, *reinterpret_cast<const QNode4*>(top.data()));
+    const QNode4* p = reinterpret_cast<const QNode4*>(w.bytes.data());
+    for (size_t i = 0; i < w.count; ++i) put(i + 1, p[i]);
+    return t;
+}
+
+// closest hit with near-first order; returns hit tri index or -1
+static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Stats& st, float& best) {
+    best = 1e30f;
+    int hit = -1;
+    std::vector<std::pair<float, int>> stack;  // (tn, code) ; code >= 0 node, < 0 leaf
+    stack.push_back({0.0f, 0});
+    size_t maxs = 0;
+    while (!stack.empty()) {
+        auto [tn0, code] = stack.back();
+        stack.pop_back();
+        if (tn0 > best) continue;
+        if (code < 0) {
+            const int v = -code - 1, first = v >> 4, cnt = v & 15;
+            st.leaves += 1;
+            for (int k = 0; k < cnt; ++k) {
+                st.tests += 1;
+                float tt;
+                if (tri_hit(tris[first + k], q, tt) && tt < best) {
+                    best = tt;
+                    hit = first + k;
+                }
+            }
+            continue;
+        }
+        st.visits += 1;
+        std::vector<std::pair<float, int>> hits;
+        for (int s = 0; s < t.W; ++s) {
+            const ChildRef& c = t.kids[(size_t)t.W * code + s];
+            if (c.count < 0) continue;
+            float tn;
+            if (!slab(c.lo, c.hi, q, best, tn)) continue;
+            hits.push_back({tn, c.count > 0 ? -(c.ref * 16 + c.count) - 1 : c.ref});
+        }
+        std::sort(hits.begin(), hits.end(), [](auto& a, auto& b) { return a.first > b.first; });
+        for (auto& h : hits) stack.push_back(h);
+        maxs = std::max(maxs, stack.size());
+    }
+    st.maxstack = std::max(st.maxstack, (double)maxs);
+    return hit;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 8) {
+        std::fprintf(stderr, "usage: bvh_stats scene.f32 n_tris ex ey ez n_rays bounces\n");
+        return 1;
+    }
+    const long n = std::atol(argv[2]);
+    std::vector<float> tv(9 * n);
+    FILE* f = std::fopen(argv[1], "rb");
+    if (!f || std::fread(tv.data(), 4, tv.size(), f) != tv.size()) return 2;
+    std::fclose(f);
+    const float em[3] = {(float)std::atof(argv[3]), (float)std::atof(argv[4]), (float)std::atof(argv[5])};
+    const int nr = std::atoi(argv[6]), nb = std::atoi(argv[7]);
+    BvhBuild b;
+    std::vector<float> ab(n, 0.5f);
+    build_bvh(tv.data(), ab.data(), 0.5f, n, 0, b);
+    relocate_bvh(b, 1, 0);
+    BvhNode top = make_node(b.root, empty_child());
+    Tree t2 = from_binary(b.nodes, top);
+    WideBuild w4, w8;
+    collapse_bvh(b, 1, 4, 1, w4);
+    collapse_bvh(b, 1, 8, 1, w8);
+    std::vector<uint8_t> top4, top8;
+    make_wide_top(4, w4.root, empty_child(), top4);
+    make_wide_top(8, w8.root, empty_child(), top8);
+    Tree t4 = from_wide<4>(top4, w4), t8 = from_wide<8>(top8, w8);
+    WideBuild wq;
+    collapse_bvh(b, 1, kWideQ4, 1, wq);
+    std::vector<uint8_t> topq;
+    make_wide_top(kWideQ4, wq.root, empty_child(), topq);
+    Tree tq = from_q4(topq, wq);
+    std::printf("tris %ld  binary nodes %zu depth %d | wide4 %zu depth %d | wide8 %zu depth %d\n", n, b.nodes.size(),
+                b.depth, w4.count, w4.depth, w8.count, w8.depth);
+    Tree* trees[4] = {&t2, &t4, &t8, &tq};
+    const double node_bytes[4] = {64, 128, 256, 64};
+    std::uniform_real_distribution<float> U(0.0f, 1.0f);
+    for (int k = 0; k < 4; ++k) {
+        Stats st;
+        long queries = 0;
+        std::mt19937 r2(7);
+        for (int i = 0; i < nr; ++i) {
+            const float z = 2 * U(r2) - 1, ph = 6.2831853f * U(r2), s = std::sqrt(1 - z * z);
+            Q q;
+            float o[3] = {em[0], em[1], em[2]}, d[3] = {s * std::cos(ph), s * std::sin(ph), z};
+            for (int bn = 0; bn < nb; ++bn) {
+                for (int a = 0; a < 3; ++a) {
+                    q.o[a] = o[a];
+                    q.d[a] = d[a];
+                    q.inv[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? 1e-20f : d[a]);
+                }
+                float tt;
+                const int h = trace(*trees[k], b.tris, q, st, tt);
+                ++queries;
+                if (h < 0) break;
+                const TriRec& tr = b.tris[h];
+                const float e1[3] = {tr.v1[0] - tr.v0[0], tr.v1[1] - tr.v0[1], tr.v1[2] - tr.v0[2]};
+                const float e2[3] = {tr.v2[0] - tr.v0[0], tr.v2[1] - tr.v0[1], tr.v2[2] - tr.v0[2]};
+                float ng[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+                const float l = std::sqrt(ng[0] * ng[0] + ng[1] * ng[1] + ng[2] * ng[2]);
+                for (float& c : ng) c /= l;
+                const float dn = 2 * (d[0] * ng[0] + d[1] * ng[1] + d[2] * ng[2]);
+                for (int a = 0; a < 3; ++a) {
+                    o[a] = o[a] + tt * d[a];
+                    d[a] -= dn * ng[a];
+                    o[a] += 1e-3f * d[a];
+                }
+            }
+        }
+        const double v = st.visits / queries, te = st.tests / queries, lv = st.leaves / queries;
+        std::printf("W=%d: %ld queries  visits %.1f  leaves %.1f  tri tests %.1f  node bytes %.0f  tri bytes %.0f  "
+                    "max stack %.0f\n",
+                    trees[k]->W, queries, v, lv, te, v * node_bytes[k], te * 48.0, st.maxstack);
+    }
+    return 0;
+}
