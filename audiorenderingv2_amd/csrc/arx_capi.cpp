@@ -51,6 +51,10 @@ arx_status fail(arx_status s, const char* fmt, ...) {
 // shared with arx_io.cpp so the loaders report through arx_last_error()
 void arx_set_last_error(const std::string& m) { g_last_error = m; }
 
+// device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4] ray cursor
+// [8..15] utilisation counters of the instrumented trace variant (98)
+constexpr int kCounters = 16;
+
 struct arx_renderer {
     arx_config cfg;
     int32_t ir_len = 0;
@@ -369,13 +373,13 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
         (e = hipEventCreate(&r->ev0)) != hipSuccess || (e = hipEventCreate(&r->ev1)) != hipSuccess ||
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&r->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipHostMalloc(&r->h_counters, 8 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
+        (e = hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc(&r->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(r->stream)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     *out = r;
@@ -504,7 +508,7 @@ arx_status arx_clear_histogram(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     ARX_HIP(hipSetDevice(r->cfg.device));
     ARX_HIP(hipMemsetAsync(r->hist(), 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream));
-    ARX_HIP(hipMemsetAsync(r->d_counters, 0, 8 * sizeof(unsigned long long), r->stream));
+    ARX_HIP(hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream));
     return ARX_OK;
 }
 
@@ -618,7 +622,7 @@ arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir
 arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     if (!r || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    ARX_HIP(hipMemcpyAsync(r->h_counters, r->d_counters, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    ARX_HIP(hipMemcpyAsync(r->h_counters, r->d_counters, kCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));
     r->stats.queries = r->h_counters[0];
@@ -628,6 +632,16 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     if (hipEventElapsedTime(&ms, r->ev0, r->ev1) == hipSuccess) r->stats.trace_ms = ms;
     *out = r->stats;
     if (r->h_counters[3]) return fail(ARX_ERR_INTERNAL, "trace kernel reported a BVH stack overflow");
+    return ARX_OK;
+}
+
+arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n) {
+    if (!r || !out || n > (size_t)kCounters) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipMemcpyAsync(r->h_counters, r->d_counters, kCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    for (size_t i = 0; i < n; ++i) out[i] = r->h_counters[i];
     return ARX_OK;
 }
 

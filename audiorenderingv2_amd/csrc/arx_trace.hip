@@ -603,8 +603,12 @@ __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, flo
     }
 }
 
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW>
+// DBG: wave-level utilisation counters in counters[8..15] (variant 98): outer iterations,
+// node-step iterations, lanes in node steps, leaf-step iterations, lanes in leaf steps,
+// lanes shading, lanes idle (active, query done) at node/leaf iterations.
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
+    uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
     __shared__ int stk[STACK * BLOCK];
     const int lane = threadIdx.x;
     const uint64_t n = a.ray_end - a.ray_begin;
@@ -629,6 +633,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     t.pc = 0;
     t.visits = 0;
     while (true) {
+        if constexpr (DBG) {
+            ++d_outer;
+            d_sh += __popcll(__ballot(active && !trav));
+        }
         if (active && !trav) {
             shade(a, s, r, t.best, n_rx, n_miss);
             if (!wants_query(a, s)) active = false;
@@ -679,16 +687,37 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             const unsigned long long m_node = __ballot(can_node);
             const unsigned long long m_leaf = __ballot(trav && t.pc > 0);
             if ((m_node | m_leaf) == 0ull) break;
-            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            const int n_idle = __popcll(__ballot(active && !trav));
+            if (n_idle >= THRESH) break;
+            if constexpr (DBG) d_idle += n_idle;
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+                if constexpr (DBG) {
+                    ++d_nit;
+                    d_nl += __popcll(m_node);
+                }
                 if (can_node) node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
             } else if (trav && t.pc > 0) {
+                if constexpr (DBG) {
+                    ++d_lit;
+                    d_ll += __popcll(m_leaf);
+                }
                 leaf_hits(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
                 t.pc = 0;
             }
         }
     }
     flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+    if constexpr (DBG) {
+        if ((lane & 63) == 0) {
+            atomicAdd(a.counters + 8, (unsigned long long)d_outer);
+            atomicAdd(a.counters + 9, (unsigned long long)d_nit);
+            atomicAdd(a.counters + 10, (unsigned long long)d_nl);
+            atomicAdd(a.counters + 11, (unsigned long long)d_lit);
+            atomicAdd(a.counters + 12, (unsigned long long)d_ll);
+            atomicAdd(a.counters + 13, (unsigned long long)d_sh);
+            atomicAdd(a.counters + 14, (unsigned long long)d_idle);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- wide tree (v4) ---
@@ -1055,11 +1084,11 @@ hipError_t launch_v2(const TraceArgs& a, int cus, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
-template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1>
+template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false>
 hipError_t launch_v3(const TraceArgs& a, int cus, hipStream_t s) {
     hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
     if (e != hipSuccess) return e;
-    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW>;
+    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
@@ -1145,6 +1174,7 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 206: return launch_v3<128, 28, 12, 32, 5>(a, cus, s);
         case 207: return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
         case 2: return launch_v2<128, 16>(a, cus, s);
+        case 98: return launch_v3<128, 32, 12, 28, 5, true>(a, cus, s);  // utilisation counters
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);

@@ -165,6 +165,10 @@ arx_status arx_prepare_ir_spectra(arx_renderer* r, int which);
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);
+/* Raw device counters of the last trace (n <= 16): [0] queries [1] receiver hits [2] misses
+ * [3] error flag [4] ray cursor; [8..14] wave-utilisation counters of the instrumented kernel
+ * variant (ARX_TRACE_KERNEL=98), see arx_trace.hip. */
+arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
 
 /* ---- Input formats (host only, no device needed) ------------------------------------------ */
 
