@@ -15,10 +15,7 @@
 namespace arx {
 namespace {
 
-constexpr int kBins = 32;
-constexpr int kLeafMax = 4;          // SAH may stop at <= kLeafMax
-constexpr float kTraversalCost = 1.0f;
-constexpr float kIntersectCost = 1.0f;
+constexpr int kMaxBins = 256;
 
 struct Prim {
     float lo[3], hi[3], c[3];
@@ -46,6 +43,7 @@ struct Box {
 };
 
 struct Builder {
+    BuildParams prm = build_params();
     std::vector<Prim> prims;
     BvhBuild* out;
     const float* tri_v;
@@ -100,16 +98,17 @@ struct Builder {
         for (int axis = 0; axis < 3; ++axis) {
             float cmin = cbounds.lo[axis], cmax = cbounds.hi[axis];
             if (!(cmax > cmin)) continue;
+            const int kBins = prm.bins;
             float scale = kBins / (cmax - cmin);
-            Box bb[kBins];
-            int64_t cnt[kBins] = {0};
+            Box bb[kMaxBins];
+            int64_t cnt[kMaxBins] = {0};
             for (int64_t i = begin; i < end; ++i) {
                 int b = std::min(kBins - 1, (int)((prims[i].c[axis] - cmin) * scale));
                 cnt[b]++;
                 bb[b].grow(prims[i].lo, prims[i].hi);
             }
-            float right_area[kBins];
-            int64_t right_cnt[kBins];
+            float right_area[kMaxBins];
+            int64_t right_cnt[kMaxBins];
             Box acc;
             int64_t ac = 0;
             for (int b = kBins - 1; b > 0; --b) {
@@ -133,12 +132,13 @@ struct Builder {
             }
         }
         float parent_area = bounds.area();
-        float sah = kTraversalCost + (parent_area > 0 ? kIntersectCost * best_cost / parent_area : 0.0f);
-        if (n <= kLeafMax && (best_axis < 0 || sah >= kIntersectCost * (float)n)) return leaf(begin, end, bounds);
+        float sah = prm.trav_cost + (parent_area > 0 ? prm.isect_cost * best_cost / parent_area : 0.0f);
+        if (n <= prm.leaf_max && (best_axis < 0 || sah >= prm.isect_cost * (float)n)) return leaf(begin, end, bounds);
 
         int64_t mid;
         if (best_axis >= 0) {
             float cmin = cbounds.lo[best_axis], cmax = cbounds.hi[best_axis];
+            const int kBins = prm.bins;
             float scale = kBins / (cmax - cmin);
             auto it = std::stable_partition(prims.begin() + begin, prims.begin() + end, [&](const Prim& p) {
                 int b = std::min(kBins - 1, (int)((p.c[best_axis] - cmin) * scale));
@@ -161,6 +161,11 @@ struct Builder {
 };
 
 }  // namespace
+
+BuildParams& build_params() {
+    static BuildParams p;
+    return p;
+}
 
 ChildRef empty_child() {
     ChildRef c;
@@ -211,7 +216,7 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
         p.idx = (int32_t)i;
     }
     b.pad = std::max(1e-5f * mx, 1e-6f);
-    out.nodes.reserve((size_t)(2 * n / kLeafMax + 16));
+    out.nodes.reserve((size_t)(2 * n / std::max(1, b.prm.leaf_max) + 16));
     out.tris.reserve((size_t)n);
     out.root = b.build(0, n, 1);
 }

@@ -22,6 +22,16 @@ struct BvhBuild {
     int depth = 0;
 };
 
+// SAH build parameters (process-wide; the defaults are the production setting, design tools
+// such as tools/bvh_stats.cpp vary them).
+struct BuildParams {
+    int bins = 32;           // centroid bins per axis (<= 256)
+    int leaf_max = 4;        // SAH may stop at <= leaf_max triangles (always splits above)
+    float trav_cost = 1.0f;  // SAH cost of a node step relative to ...
+    float isect_cost = 1.0f; // ... one triangle test
+};
+BuildParams& build_params();
+
 // tri_v: n*9 floats, tri_abs: n floats (may be nullptr -> absorption_fill).
 void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, int64_t n, int32_t id_base,
                BvhBuild& out);

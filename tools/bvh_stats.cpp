@@ -183,6 +183,12 @@ int main(int argc, char** argv) {
     std::fclose(f);
     const float em[3] = {(float)std::atof(argv[3]), (float)std::atof(argv[4]), (float)std::atof(argv[5])};
     const int nr = std::atoi(argv[6]), nb = std::atoi(argv[7]);
+    BuildParams& bp = build_params();
+    if (const char* e = std::getenv("BINS")) bp.bins = std::atoi(e);
+    if (const char* e = std::getenv("LEAF")) bp.leaf_max = std::atoi(e);
+    if (const char* e = std::getenv("TRAV")) bp.trav_cost = (float)std::atof(e);
+    if (const char* e = std::getenv("ISECT")) bp.isect_cost = (float)std::atof(e);
+    std::printf("params: bins %d leaf_max %d trav %.2f isect %.2f\n", bp.bins, bp.leaf_max, bp.trav_cost, bp.isect_cost);
     BvhBuild b;
     std::vector<float> ab(n, 0.5f);
     build_bvh(tv.data(), ab.data(), 0.5f, n, 0, b);
