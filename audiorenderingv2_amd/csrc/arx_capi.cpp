@@ -52,7 +52,8 @@ arx_status fail(arx_status s, const char* fmt, ...) {
 void arx_set_last_error(const std::string& m) { g_last_error = m; }
 
 // device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4] ray cursor
-// [8..15] utilisation counters of the instrumented trace variant (98)
+// [6..7] parked-ray counts of the phased launches, [8..15] utilisation counters of the
+// instrumented trace variant (98)
 constexpr int kCounters = 16;
 
 struct arx_renderer {
@@ -89,6 +90,7 @@ struct arx_renderer {
     int32_t* d_spill = nullptr;
     size_t spill_cap = 0;   // int32 entries
     int32_t stack_need = 0;
+    uint8_t* d_stash = nullptr;  // phased-launch ray stash (2 x lanes x 48 B)
     unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
     unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
     unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
@@ -398,6 +400,7 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_tris);
     hipFree(r->d_wnodes);
     hipFree(r->d_spill);
+    hipFree(r->d_stash);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
@@ -550,6 +553,15 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.spill = r->d_spill;
     a.spill_lanes = trace_spill_lanes(r->cus);
     a.stack_need = r->stack_need;
+    if (!r->d_stash) {  // parked-ray buffers of the phased launches: 48 B per lane, two of them
+        const size_t bytes = 2 * trace_spill_lanes(r->cus) * 48;
+        ARX_HIP(hipMalloc(&r->d_stash, bytes));
+    }
+    a.stash[0] = r->d_stash;
+    a.stash[1] = r->d_stash + trace_spill_lanes(r->cus) * 48;
+    a.stash_count = r->d_counters + 6;
+    a.stash_cap = trace_spill_lanes(r->cus);
+    a.pool_from = -1;
     if (ray_end == ray_begin) return ARX_OK;
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream));

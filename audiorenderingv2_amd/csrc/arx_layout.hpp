@@ -103,6 +103,14 @@ struct TraceArgs {
     uint64_t spill_lanes;
     int32_t stack_need;  // worst-case stack entries for this tree: (W-1) * wide depth + 2
     int32_t spill_depth; // set by the launcher: stack_need - LDS entries (>= 0)
+    // phased launches (tail compaction): ray states parked between launches, 48 B each:
+    // float4(pos, e), float4(dir, dist), int4(depth, 0, 0, 0)
+    void* stash[2];
+    unsigned long long* stash_count;  // [2] device counters
+    uint64_t stash_cap;               // records per stash buffer
+    // set by the launcher per phase: source pool (-1 = fresh ray ids) and drain threshold
+    int32_t pool_from;   // -1 or 0/1: read states from stash[pool_from]
+    int32_t drain_low;   // 0: never drain; else drain a wave once exhausted with < drain_low active lanes
 };
 
 }  // namespace arx

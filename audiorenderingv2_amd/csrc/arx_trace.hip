@@ -606,12 +606,60 @@ __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, flo
 // DBG: wave-level utilisation counters in counters[8..15] (variant 98): outer iterations,
 // node-step iterations, lanes in node steps, leaf-step iterations, lanes in leaf steps,
 // lanes shading, lanes idle (active, query done) at node/leaf iterations.
+// Parked ray state (phased launches): float4(pos, e), float4(dir, dist), int4(depth, 0, 0, 0).
+__device__ __forceinline__ void park_ray(const TraceArgs& a, int to, uint64_t slot, const RayState& s) {
+    float4* rec = reinterpret_cast<float4*>(a.stash[to]) + 3 * slot;
+    rec[0] = make_float4(s.pos.x, s.pos.y, s.pos.z, s.e);
+    rec[1] = make_float4(s.dir.x, s.dir.y, s.dir.z, s.dist);
+    rec[2] = make_float4(__int_as_float(s.depth), 0.0f, 0.0f, 0.0f);
+}
+
+__device__ __forceinline__ void unpark_ray(const TraceArgs& a, uint64_t slot, RayState& s) {
+    const float4* rec = reinterpret_cast<const float4*>(a.stash[a.pool_from]) + 3 * slot;
+    const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+    s.pos = make_float3(r0.x, r0.y, r0.z);
+    s.e = r0.w;
+    s.dir = make_float3(r1.x, r1.y, r1.z);
+    s.dist = r1.w;
+    s.depth = __float_as_int(r2.x);
+}
+
+// Phase drain (wave-uniform): once the pool is exhausted and fewer than drain_low lanes still
+// hold rays, the wave parks every ray that sits at a query boundary into the next phase's
+// stash; the wave ends when its last in-flight query has been parked.
+__device__ __forceinline__ void drain_wave(const TraceArgs& a, bool exhausted, bool trav, bool& active,
+                                           bool& draining, const RayState& s, int lane, bool& overflow) {
+    if (a.drain_low <= 0 || !exhausted) return;
+    if (!draining && __popcll(__ballot(active)) < a.drain_low) draining = true;
+    if (!draining) return;
+    const unsigned long long park = __ballot(active && !trav);
+    if (park == 0ull) return;
+    const int to = a.pool_from < 0 ? 0 : 1 - a.pool_from;
+    const int leader = __ffsll((unsigned long long)park) - 1;
+    unsigned long long base = 0;
+    if ((lane & 63) == leader) base = atomicAdd(a.stash_count + to, (unsigned long long)__popcll(park));
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+    base = ((unsigned long long)hi << 32) | lo;
+    if (active && !trav) {
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(park >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)park, 0u));
+        if (base + rank < a.stash_cap) {
+            park_ray(a, to, base + rank, s);
+            active = false;
+        } else {
+            overflow = true;  // cannot happen with stash_cap >= lanes of the grid; keep the ray
+        }
+    }
+}
+
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
     __shared__ int stk[STACK * BLOCK];
     const int lane = threadIdx.x;
-    const uint64_t n = a.ray_end - a.ray_begin;
+    const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
+    bool draining = false;
     unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
     bool overflow = false;
@@ -641,6 +689,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             shade(a, s, r, t.best, n_rx, n_miss);
             if (!wants_query(a, s)) active = false;
         }
+        drain_wave(a, exhausted, trav, active, draining, s, lane, overflow);
         const unsigned long long need = __ballot(!active);
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
@@ -655,7 +704,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint64_t i = base + rank;
                 if (i < n) {
-                    ray_init(a, s, a.ray_begin + i);
+                    if (a.pool_from < 0)
+                        ray_init(a, s, a.ray_begin + i);
+                    else
+                        unpark_ray(a, i, s);
                     active = wants_query(a, s);
                 }
             }
@@ -1084,14 +1136,38 @@ hipError_t launch_v2(const TraceArgs& a, int cus, hipStream_t s) {
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
+int env_int(const char* name, int def) {
+    const char* v = getenv(name);
+    return (v && v[0]) ? atoi(v) : def;
+}
+
+// Tail compaction: phase 0 traces fresh ray ids; once a wave runs dry it parks its in-flight
+// rays (at query boundaries) into a stash and exits, and the next phase refills full waves from
+// that stash.  The last phase runs to completion.  Counts live on the device, so the phases
+// are enqueued back to back without host synchronisation; empty phases exit immediately.
 template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false>
-hipError_t launch_v3(const TraceArgs& a, int cus, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
-    if (e != hipSuccess) return e;
+hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
+    TraceArgs a = args;
     auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
-    return hipGetLastError();
+    const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 4)) : 1;
+    const int low = env_int("ARX_DRAIN_LOW", 32);
+    if ((uint64_t)grid * BLOCK > a.stash_cap && phases > 1) return hipErrorInvalidValue;
+    for (int p = 0; p < phases; ++p) {
+        a.pool_from = p == 0 ? -1 : (p - 1) % 2;
+        a.drain_low = (p + 1 < phases) ? low : 0;
+        hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
+        if (e != hipSuccess) return e;
+        if (a.drain_low > 0) {
+            const int to = a.pool_from < 0 ? 0 : 1 - a.pool_from;
+            e = hipMemsetAsync(a.stash_count + to, 0, sizeof(unsigned long long), s);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW>
 hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
