@@ -215,6 +215,41 @@ __device__ __forceinline__ void leaf_hits(const TriRec* __restrict__ tris, const
     }
 }
 
+// Leaf test with the loads of V triangles in flight together.  Slots past the leaf's end are
+// clamped to its last triangle: re-testing a triangle cannot change the (t, id) minimum.
+template <int V>
+__device__ __forceinline__ void leaf_hits_vec(const TriRec* __restrict__ tris, const Ray& r, int first, int count,
+                                              float& best_t, int& best_id, int& best) {
+    if constexpr (V == 1) {
+        leaf_hits(tris, r, first, count, best_t, best_id, best);
+    } else {
+        for (int k = 0; k < count; k += V) {
+            float4 p[V][3];
+            int idx[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                idx[j] = first + min(k + j, count - 1);
+                const float4* tp = reinterpret_cast<const float4*>(tris + idx[j]);
+                p[j][0] = tp[0];
+                p[j][1] = tp[1];
+                p[j][2] = tp[2];
+            }
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                Hit h;
+                if (tri_test(r, p[j][0], p[j][1], p[j][2], h)) {
+                    const int id = __float_as_int(p[j][1].w);
+                    if (h.t < best_t || (h.t == best_t && id < best_id)) {
+                        best_t = h.t;
+                        best_id = id;
+                        best = idx[j];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Per-lane traversal state of one closest-hit query over the two-level BVH (node 0 = top).
 struct Trav {
     float best_t;
@@ -653,7 +688,7 @@ __device__ __forceinline__ void drain_wave(const TraceArgs& a, bool exhausted, b
     }
 }
 
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false>
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
     __shared__ int stk[STACK * BLOCK];
@@ -753,7 +788,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     ++d_lit;
                     d_ll += __popcll(m_leaf);
                 }
-                leaf_hits(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
+                leaf_hits_vec<LV>(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
                 t.pc = 0;
             }
         }
@@ -1145,12 +1180,12 @@ int env_int(const char* name, int def) {
 // rays (at query boundaries) into a stash and exits, and the next phase refills full waves from
 // that stash.  The last phase runs to completion.  Counts live on the device, so the phases
 // are enqueued back to back without host synchronisation; empty phases exit immediately.
-template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false>
+template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false, int LV = 1>
 hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     TraceArgs a = args;
-    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG>;
+    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
-    const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 4)) : 1;
+    const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 1)) : 1;
     const int low = env_int("ARX_DRAIN_LOW", 32);
     if ((uint64_t)grid * BLOCK > a.stash_cap && phases > 1) return hipErrorInvalidValue;
     for (int p = 0; p < phases; ++p) {
@@ -1251,6 +1286,13 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 207: return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
         case 2: return launch_v2<128, 16>(a, cus, s);
         case 98: return launch_v3<128, 32, 12, 28, 5, true>(a, cus, s);  // utilisation counters
+        // triangle loads of 2 / 4 leaf triangles in flight together
+        case 400: return launch_v3<128, 32, 12, 28, 5, false, 2>(a, cus, s);
+        case 401: return launch_v3<128, 32, 12, 28, 5, false, 4>(a, cus, s);
+        case 402: return launch_v3<128, 32, 8, 28, 5, false, 2>(a, cus, s);
+        case 403: return launch_v3<128, 32, 16, 28, 5, false, 2>(a, cus, s);
+        case 404: return launch_v3<128, 24, 12, 28, 5, false, 2>(a, cus, s);
+        case 405: return launch_v3<128, 32, 12, 28, 4, false, 2>(a, cus, s);
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
