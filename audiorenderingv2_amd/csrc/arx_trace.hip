@@ -691,6 +691,8 @@ __device__ __forceinline__ void drain_wave(const TraceArgs& a, bool exhausted, b
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
+    uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
+    if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
     __shared__ int stk[STACK * BLOCK];
     const int lane = threadIdx.x;
     const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
@@ -768,6 +770,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             if (exhausted) break;
             continue;
         }
+        if constexpr (DBG) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            c_outer += now - c_mark;
+            c_mark = now;
+        }
         while (true) {
             if (trav && t.pc == 0 && t.node < 0 && t.sp == 0) trav = false;  // query finished
             const bool can_node = trav && t.pc == 0;
@@ -783,13 +790,25 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     d_nl += __popcll(m_node);
                 }
                 if (can_node) node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
-            } else if (trav && t.pc > 0) {
+                if constexpr (DBG) {
+                    const uint64_t now = __builtin_amdgcn_s_memtime();
+                    c_node += now - c_mark;
+                    c_mark = now;
+                }
+            } else {
                 if constexpr (DBG) {
                     ++d_lit;
                     d_ll += __popcll(m_leaf);
                 }
-                leaf_hits_vec<LV>(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
-                t.pc = 0;
+                if (trav && t.pc > 0) {
+                    leaf_hits_vec<LV>(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
+                    t.pc = 0;
+                }
+                if constexpr (DBG) {
+                    const uint64_t now = __builtin_amdgcn_s_memtime();
+                    c_leaf += now - c_mark;
+                    c_mark = now;
+                }
             }
         }
     }
@@ -803,6 +822,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             atomicAdd(a.counters + 12, (unsigned long long)d_ll);
             atomicAdd(a.counters + 13, (unsigned long long)d_sh);
             atomicAdd(a.counters + 14, (unsigned long long)d_idle);
+            atomicAdd(a.counters + 5, (unsigned long long)c_node);
+            atomicAdd(a.counters + 15, (unsigned long long)c_leaf);
+            atomicAdd(a.counters + 7, (unsigned long long)c_outer);
         }
     }
 }

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Wave-utilisation report of the trace kernel (instrumented variant 98 = default v3 + counters).
 
+Counters [8..14] + s_memtime cycles in [5] (node), [15] (leaf), [7] (outer).
 Lane utilisation of a phase = lanes doing that phase's work / (iterations x 64)."""
 import ctypes as C
 import os
@@ -27,3 +28,7 @@ print(f"node steps: {nit} wave-iterations, {nl} lane-steps = {nl / q:.1f} per qu
 print(f"leaf steps: {lit} wave-iterations, {ll} lane-steps = {ll / q:.1f} per query, utilisation {ll / (64 * max(lit, 1)):.3f}")
 print(f"idle lanes per inner iteration {idle / max(nit + lit, 1):.1f} of 64")
 print(f"wave-iterations per query: node {nit / q:.3f} leaf {lit / q:.3f} outer {outer / q:.3f}")
+cn, cl, co = c[5], c[15], c[7]
+tot = cn + cl + co
+print(f"wave cycles (s_memtime): node {cn / tot:.3f}  leaf {cl / tot:.3f}  outer/shade/refill {co / tot:.3f}")
+print(f"cycles per wave-iteration: node {cn / max(nit, 1):.0f}  leaf {cl / max(lit, 1):.0f}  outer {co / max(outer, 1):.0f}")
