@@ -250,6 +250,67 @@ __device__ __forceinline__ void leaf_hits_vec(const TriRec* __restrict__ tris, c
     }
 }
 
+// Branch-free watertight test: same arithmetic and result as tri_test, decided by selects.
+__device__ __forceinline__ bool tri_test_nb(const Ray& r, float4 p0, float4 p1, float4 p2, float& t_out) {
+    const float Ax = sel3(p0.x, p0.y, p0.z, r.kx) - r.op[0];
+    const float Ay = sel3(p0.x, p0.y, p0.z, r.ky) - r.op[1];
+    const float Az = sel3(p0.x, p0.y, p0.z, r.kz) - r.op[2];
+    const float Bx = sel3(p1.x, p1.y, p1.z, r.kx) - r.op[0];
+    const float By = sel3(p1.x, p1.y, p1.z, r.ky) - r.op[1];
+    const float Bz = sel3(p1.x, p1.y, p1.z, r.kz) - r.op[2];
+    const float Cx = sel3(p2.x, p2.y, p2.z, r.kx) - r.op[0];
+    const float Cy = sel3(p2.x, p2.y, p2.z, r.ky) - r.op[1];
+    const float Cz = sel3(p2.x, p2.y, p2.z, r.kz) - r.op[2];
+    const float ax = Ax - r.sx * Az;
+    const float ay = Ay - r.sy * Az;
+    const float bx = Bx - r.sx * Bz;
+    const float by = By - r.sy * Bz;
+    const float cx = Cx - r.sx * Cz;
+    const float cy = Cy - r.sy * Cz;
+    const float U = cx * by - cy * bx;
+    const float V = ax * cy - ay * cx;
+    const float W = bx * ay - by * ax;
+    const bool mixed = (U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f);
+    const float det = U + V + W;
+    const float az = r.sz * Az;
+    const float bz = r.sz * Bz;
+    const float cz = r.sz * Cz;
+    const float T = U * az + V * bz + W * cz;
+    const float t = T / det;
+    t_out = t;
+    return !mixed && det != 0.0f && t >= 0.0f;
+}
+
+// Leaf step without divergent control flow: the trip count is the wave's largest pending
+// leaf (uniform), lanes with shorter or no leaves re-test a clamped slot (cannot change the
+// (t, id) minimum) or a dummy triangle whose result is discarded.
+template <int V>
+__device__ __forceinline__ void leaf_hits_u(const TriRec* __restrict__ tris, const Ray& r, int first, int count,
+                                            float& best_t, int& best_id, int& best) {
+    for (int k = 0; __ballot(k < count) != 0ull; k += V) {
+        float4 p[V][3];
+        int idx[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            idx[j] = count > 0 ? first + min(k + j, count - 1) : 0;
+            const float4* tp = reinterpret_cast<const float4*>(tris + idx[j]);
+            p[j][0] = tp[0];
+            p[j][1] = tp[1];
+            p[j][2] = tp[2];
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            float th;
+            const bool hit = tri_test_nb(r, p[j][0], p[j][1], p[j][2], th) && count > 0;
+            const int id = __float_as_int(p[j][1].w);
+            const bool better = hit && (th < best_t || (th == best_t && id < best_id));
+            best_t = better ? th : best_t;
+            best_id = better ? id : best_id;
+            best = better ? idx[j] : best;
+        }
+    }
+}
+
 // Per-lane traversal state of one closest-hit query over the two-level BVH (node 0 = top).
 struct Trav {
     float best_t;
@@ -688,12 +749,78 @@ __device__ __forceinline__ void drain_wave(const TraceArgs& a, bool exhausted, b
     }
 }
 
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1>
+// Branch-free node step (same traversal order as node_step3).  Divergent `if`s cost scalar
+// exec-mask bookkeeping that one scalar unit per CU executes for all 20 waves -- the node
+// loop was bound by it -- so every decision here is a v_cndmask and the stack is written
+// unconditionally (to a dummy row STACK when nothing is pushed).  Requires stk[(STACK+1)*BLOCK].
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void node_step5(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, bool& overflow) {
+    // pop (lanes whose next node is on the stack); a popped leaf becomes the pending leaf
+    const bool do_pop = t.node < 0;
+    const int sp_pop = t.sp - 1;
+    const int e = stk[(do_pop ? sp_pop : STACK) * BLOCK + lane];
+    t.sp = do_pop ? sp_pop : t.sp;
+    const bool got_leaf = do_pop && e < 0;
+    const int ne = ~e;  // -(first*16 + count) - 1 -> first*16 + count
+    t.pf = got_leaf ? (ne >> 4) : t.pf;
+    t.pc = got_leaf ? (ne & 15) : t.pc;
+    const int node = do_pop ? (got_leaf ? 0 : e) : t.node;  // got_leaf: harmless visit of node 0, discarded
+    const float4* np = reinterpret_cast<const float4*>(a.nodes + node);
+    const float4 na = np[0];
+    const float4 nb = np[1];
+    const float4 nc = np[2];
+    const int4 nd = *reinterpret_cast<const int4*>(np + 3);
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = !got_leaf && tn0 <= tf0 && nd.z >= 0;
+    const bool h1 = !got_leaf && tn1 <= tf1 && nd.w >= 0;
+    const bool l0 = h0 && nd.z > 0, l1 = h1 && nd.w > 0;
+    const bool i0 = h0 && nd.z == 0, i1 = h1 && nd.w == 0;
+    const bool swap = tn1 < tn0;
+    // leaves: the nearer hit leaf is parked, a second one pushed
+    const bool two_l = l0 && l1;
+    const bool near_is1 = two_l ? swap : l1;
+    const bool any_l = l0 || l1;
+    t.pf = any_l ? (near_is1 ? nd.y : nd.x) : t.pf;
+    t.pc = any_l ? (near_is1 ? nd.w : nd.z) : t.pc;
+    {
+        const int code = swap ? leaf_code(nd.x, nd.z) : leaf_code(nd.y, nd.w);
+        const bool fits = t.sp < STACK;
+        overflow = overflow || (two_l && !fits);
+        const bool push = two_l && fits;
+        stk[(push ? t.sp : STACK) * BLOCK + lane] = code;
+        t.sp += push ? 1 : 0;
+    }
+    // inner children: visit the nearer, push the other
+    const bool two_i = i0 && i1;
+    {
+        const int far_n = swap ? nd.x : nd.y;
+        const bool fits = t.sp < STACK;
+        overflow = overflow || (two_i && !fits);
+        const bool push = two_i && fits;
+        stk[(push ? t.sp : STACK) * BLOCK + lane] = far_n;
+        t.sp += push ? 1 : 0;
+    }
+    const int next = two_i ? (swap ? nd.y : nd.x) : (i0 ? nd.x : (i1 ? nd.y : -1));
+    t.node = got_leaf ? -1 : next;
+}
+
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1, int NS = 3>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
     uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
     if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
-    __shared__ int stk[STACK * BLOCK];
+    __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
     const int lane = threadIdx.x;
     const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
     bool draining = false;
@@ -789,7 +916,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     ++d_nit;
                     d_nl += __popcll(m_node);
                 }
-                if (can_node) node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                if (can_node) {
+                    if constexpr (NS == 5)
+                        node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    else
+                        node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                }
                 if constexpr (DBG) {
                     const uint64_t now = __builtin_amdgcn_s_memtime();
                     c_node += now - c_mark;
@@ -800,7 +932,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     ++d_lit;
                     d_ll += __popcll(m_leaf);
                 }
-                if (trav && t.pc > 0) {
+                if constexpr (NS == 5) {
+                    const bool mine = trav && t.pc > 0;
+                    leaf_hits_u<LV>(a.tris, r, t.pf, mine ? t.pc : 0, t.best_t, t.best_id, t.best);
+                    t.pc = mine ? 0 : t.pc;
+                } else if (trav && t.pc > 0) {
                     leaf_hits_vec<LV>(a.tris, r, t.pf, t.pc, t.best_t, t.best_id, t.best);
                     t.pc = 0;
                 }
@@ -1202,10 +1338,11 @@ int env_int(const char* name, int def) {
 // rays (at query boundaries) into a stash and exits, and the next phase refills full waves from
 // that stash.  The last phase runs to completion.  Counts live on the device, so the phases
 // are enqueued back to back without host synchronisation; empty phases exit immediately.
-template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false, int LV = 1>
+template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false, int LV = 1,
+          int NS = 3>
 hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     TraceArgs a = args;
-    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV>;
+    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
     const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 1)) : 1;
     const int low = env_int("ARX_DRAIN_LOW", 32);
@@ -1315,6 +1452,18 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 403: return launch_v3<128, 32, 16, 28, 5, false, 2>(a, cus, s);
         case 404: return launch_v3<128, 24, 12, 28, 5, false, 2>(a, cus, s);
         case 405: return launch_v3<128, 32, 12, 28, 4, false, 2>(a, cus, s);
+        // branch-free node step + uniform leaf loop (NS = 5)
+        case 500: return launch_v3<128, 32, 12, 28, 5, false, 1, 5>(a, cus, s);
+        case 501: return launch_v3<128, 32, 12, 28, 5, false, 2, 5>(a, cus, s);
+        case 502: return launch_v3<128, 32, 8, 28, 5, false, 1, 5>(a, cus, s);
+        case 503: return launch_v3<128, 32, 16, 28, 5, false, 1, 5>(a, cus, s);
+        case 504: return launch_v3<128, 32, 24, 28, 5, false, 1, 5>(a, cus, s);
+        case 505: return launch_v3<128, 32, 12, 28, 4, false, 1, 5>(a, cus, s);
+        case 506: return launch_v3<128, 32, 12, 28, 6, false, 1, 5>(a, cus, s);
+        case 507: return launch_v3<128, 24, 12, 28, 5, false, 1, 5>(a, cus, s);
+        case 508: return launch_v3<128, 40, 12, 28, 5, false, 1, 5>(a, cus, s);
+        case 509: return launch_v3<64, 32, 12, 28, 5, false, 1, 5>(a, cus, s);
+        case 598: return launch_v3<128, 32, 12, 28, 5, true, 1, 5>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);

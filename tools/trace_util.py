@@ -8,7 +8,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["ARX_TRACE_KERNEL"] = "98"
+os.environ["ARX_TRACE_KERNEL"] = os.environ.get("UTIL_VARIANT", "98")
 from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local  # noqa: E402
 from audiorenderingv2_amd._lib import check, lib  # noqa: E402
 from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  # noqa: E402
