@@ -12,6 +12,7 @@
 // without a full reload().
 #pragma once
 
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
 #include <stdexcept>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "arx.h"
+#include "arx_circular_buffer.hpp"
 
 namespace arx {
 
@@ -129,6 +131,42 @@ class AudioRenderer {
         convoluteAudioFile(audio, bytes, outL, outR);
     }
 
+    // :29 -- one mic block (f64, bytes) convolved with both IRs; 2*ir_len zipped L/R values are
+    // added into the caller's CircularBuffer (AudioRenderer.cpp:593-661)
+    void convoluteLiveInput(double* h_inputBuffer, size_t h_inputBufferSize, CircularBuffer<double>* samplesRecordBuffer) {
+        live_scratch_.resize(2 * ir_length_);
+        check(arx_convolute_live_block(h_, h_inputBuffer, h_inputBufferSize, live_scratch_.data(), live_scratch_.size()));
+        if (samplesRecordBuffer) samplesRecordBuffer->add(live_scratch_.data(), live_scratch_.size());
+    }
+
+    // text dumps (AudioRenderer.cpp:525-567, 720-744; setters :780-788): the next render writes
+    // output_ir_{left,right}.txt, the next file convolution output_convolute_{left,right}.txt
+    void set_write_ir_to_file_flag(bool v) { write_ir_ = v; }
+    void set_write_output_to_file_flag(bool v) { write_output_ = v; }
+    void enable_experimentation() { experimentation_ = true; }
+    void renderWithDumps(double* render_time = nullptr) {
+        render(render_time);
+        if (!write_ir_) return;
+        std::vector<float> l(ir_length_), r(ir_length_);
+        getIR(l.data(), r.data());
+        std::string lp = "output_ir_left.txt", rp = "output_ir_right.txt";
+        if (experimentation_) {
+            const std::string stamp = std::to_string(std::chrono::system_clock::now().time_since_epoch().count());
+            lp = "experimentation/output_ir_left_" + stamp + ".txt";
+            rp = "experimentation/output_ir_right_" + stamp + ".txt";
+        }
+        check(arx_write_float_lines(lp.c_str(), l.data(), l.size()));
+        check(arx_write_float_lines(rp.c_str(), r.data(), r.size()));
+        write_ir_ = false;
+    }
+    void convoluteAudioFileWithDumps(float* in, size_t bytes, float* outL, float* outR) {
+        convoluteAudioFile(in, bytes, outL, outR);
+        if (!write_output_) return;
+        check(arx_write_float_lines("output_convolute_left.txt", outL, bytes / sizeof(float)));
+        check(arx_write_float_lines("output_convolute_right.txt", outR, bytes / sizeof(float)));
+        write_output_ = false;
+    }
+
     void getIR(float* left, float* right) { check(arx_copy_ir(h_, left, right, ir_length_)); }
     arx_stats stats() {
         arx_stats s;
@@ -141,6 +179,103 @@ class AudioRenderer {
   private:
     arx_renderer* h_ = nullptr;
     size_t ir_length_ = 0;
+    std::vector<double> live_scratch_;
+    bool write_ir_ = false, write_output_ = false, experimentation_ = false;
 };
+
+// ---- input / output formats over libarx.so's native readers ------------------------------
+
+// loadOBJ (OptixModel.cpp:75-151): one Mesh per (shape, material), names = material names.
+inline std::vector<Mesh> loadOBJ(const std::string& path) {
+    arx_model* m = nullptr;
+    check(arx_model_load_obj(path.c_str(), nullptr, 0, nullptr, &m));
+    std::vector<Mesh> out;
+    for (int64_t i = 0; i < arx_model_mesh_count(m); ++i) {
+        const char* name = nullptr;
+        const float* v = nullptr;
+        const int32_t* idx = nullptr;
+        int64_t nv = 0, nt = 0;
+        const arx_status st = arx_model_mesh(m, i, &name, &v, &nv, &idx, &nt);
+        if (st != ARX_OK) {
+            arx_model_free(m);
+            check(st);
+        }
+        Mesh mesh;
+        mesh.material_name = name ? name : "";
+        mesh.vertex.assign(v, v + 3 * nv);
+        mesh.index.assign(idx, idx + 3 * nt);
+        out.push_back(std::move(mesh));
+    }
+    arx_model_free(m);
+    return out;
+}
+
+// HalfSphere(objFile) + place_receiver_half's mesh of shapes[0] (HalfSphere.cpp:3-31,
+// OptixModel.cpp:197-220), local frame; the last material mesh wins like the reference.
+inline Mesh loadHalfSphere(const std::string& path, bool left) {
+    arx_model* m = nullptr;
+    const std::string dir = path.substr(0, path.rfind('/'));
+    check(arx_model_load_obj(path.c_str(), dir.c_str(), 1, left ? "receiver_left" : "receiver_right", &m));
+    Mesh mesh;
+    const int64_t n = arx_model_mesh_count(m);
+    if (n > 0) {
+        const char* name = nullptr;
+        const float* v = nullptr;
+        const int32_t* idx = nullptr;
+        int64_t nv = 0, nt = 0;
+        arx_model_mesh(m, n - 1, &name, &v, &nv, &idx, &nt);
+        mesh.material_name = name;
+        mesh.vertex.assign(v, v + 3 * nv);
+        mesh.index.assign(idx, idx + 3 * nt);
+    }
+    arx_model_free(m);
+    return mesh;
+}
+
+// AudioFile<float> load / save (AudioFile.h): samples[channel][frame]
+struct Wav {
+    std::vector<std::vector<float>> samples;
+    int32_t sample_rate = 44100;
+    int32_t bit_depth = 16;
+};
+
+inline Wav loadWav(const std::string& path) {
+    float* data = nullptr;
+    int32_t ch = 0, sr = 0, bits = 0;
+    int64_t n = 0;
+    check(arx_wav_load(path.c_str(), &data, &ch, &n, &sr, &bits));
+    Wav w;
+    w.sample_rate = sr;
+    w.bit_depth = bits;
+    for (int32_t c = 0; c < ch; ++c) w.samples.emplace_back(data + (size_t)c * n, data + (size_t)(c + 1) * n);
+    arx_free(data);
+    return w;
+}
+
+inline void saveWav(const std::string& path, const Wav& w) {
+    const size_t n = w.samples.empty() ? 0 : w.samples[0].size();
+    std::vector<float> flat;
+    for (const auto& c : w.samples) flat.insert(flat.end(), c.begin(), c.end());
+    check(arx_wav_save(path.c_str(), flat.data(), (int32_t)w.samples.size(), (int64_t)n, w.sample_rate, w.bit_depth));
+}
+
+// normalizeToRangeMinusOneToOne (main.cpp:628-651)
+inline std::vector<float> normalizeToRangeMinusOneToOne(std::vector<float> v) {
+    check(arx_normalize_min_max(v.data(), v.size()));
+    return v;
+}
+
+// Context::loadContext's parameters (Context.cpp:15-164); materials as the renderer takes them
+inline arx_app_config loadConfig(const std::string& path) {
+    arx_app_config c;
+    check(arx_load_app_config(path.c_str(), &c));
+    return c;
+}
+
+inline std::vector<Material> configMaterials(const arx_app_config& c) {
+    std::vector<Material> m;
+    for (int32_t i = 0; i < c.n_materials; ++i) m.push_back({c.material_names[i], c.material_absorption[i]});
+    return m;
+}
 
 }  // namespace arx

@@ -75,7 +75,8 @@ CPP = r"""
 #include "arx_audio_renderer.hpp"
 #include "arx_circular_buffer.hpp"
 #include "arx_rtaudio.hpp"
-int main() {
+int main(int argc, char** argv) {
+    (void)argc;
     arx::CircularBuffer<double> cb(7);
     std::vector<double> a = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10};
     cb.add(a.data(), a.size());
@@ -93,6 +94,16 @@ int main() {
     for (double v : out) std::printf("%g ", v);
     arx_config c; arx_default_config(&c);
     std::printf("%d\n", c.rays_x);
+    // native formats through the shim (host only)
+    auto meshes = arx::loadOBJ(argv[1]);
+    std::printf("%zu %s %zu\n", meshes.size(), meshes[0].material_name.c_str(), meshes[0].index.size() / 3);
+    arx::Wav w;
+    w.samples = {{0.5f, -0.25f, 1.0f}};
+    w.sample_rate = 8000;
+    w.bit_depth = 32;
+    arx::saveWav(argv[2], w);
+    auto r = arx::loadWav(argv[2]);
+    std::printf("%d %d %g %g\n", r.sample_rate, r.bit_depth, r.samples[0][1], arx::normalizeToRangeMinusOneToOne(r.samples[0])[0]);
     return 0;
 }
 """
@@ -105,7 +116,13 @@ def test_cpp_headers_compile_and_agree(tmp_path):
     pkg = os.path.join(REPO, "audiorenderingv2_amd")
     subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(REPO, "include"), str(src), "-L", pkg, "-larx",
                     f"-Wl,-rpath,{pkg}", "-o", str(exe)], check=True)
-    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    (tmp_path / "m.mtl").write_text("newmtl brick\n")
+    (tmp_path / "m.obj").write_text("mtllib m.mtl\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nusemtl brick\nf 1 2 3 4\n")
+    lines = subprocess.run([str(exe), str(tmp_path / "m.obj"), str(tmp_path / "w.wav")], check=True,
+                           capture_output=True, text=True).stdout.splitlines()
+    assert lines[-2].split() == ["1", "brick", "2"]
+    assert lines[-1].split() == ["8000", "32", "-0.25", "0.2"]
+    out = " ".join(lines[:-2]).split()
     vals = [float(v) for v in out]
     ops = [("add", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10]), ("get", 3), ("add", [1, 2, 3, 4]), ("get", 7)]
     ref = reference_circular(7, ops)
