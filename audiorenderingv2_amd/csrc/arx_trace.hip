@@ -815,6 +815,138 @@ __device__ __forceinline__ void node_step5(const TraceArgs& a, const Ray& r, flo
     t.node = got_leaf ? -1 : next;
 }
 
+// ---- quad-cooperative node fetch -------------------------------------------------------
+// The vector-memory return path charges per distinct 64-B block per wave-instruction
+// (tools/td_microbench.hip: a divergent dwordx4 with 64 distinct blocks costs ~4x one whose
+// quads share blocks).  Fetching a 64-B node as 4 per-lane dwordx4 loads therefore pays for
+// the node's block 4 times.  Here load k makes the 4 lanes of a quad read the 4 chunks of
+// quad-member k's node (one block per quad), and a 2-round DPP transpose (xor 1, xor 2
+// within the quad) hands every lane its own node.  Must run with all 64 lanes active;
+// lanes without a node pass node 0 and discard the result.
+__device__ __forceinline__ int dpp_bcast(int v, int k) {
+    switch (k) {  // quad_perm [k,k,k,k]
+        case 0: return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);
+        case 1: return __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);
+        case 2: return __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);
+        default: return __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);
+    }
+}
+
+template <int XOR>
+__device__ __forceinline__ int dpp_xor(int v) {  // quad_perm [1,0,3,2] / [2,3,0,1]
+    return __builtin_amdgcn_mov_dpp(v, XOR == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+}
+
+struct Chunk {
+    int v[4];
+};
+
+__device__ __forceinline__ void coop_fetch_node(const BvhNode* __restrict__ nodes, int node, int lane, float4& na,
+                                                float4& nb, float4& nc, int4& nd) {
+    const int q = lane & 3;
+    Chunk R[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int src = dpp_bcast(node, k);
+        const int4 x = reinterpret_cast<const int4*>(nodes + src)[q];
+        R[k].v[0] = x.x;
+        R[k].v[1] = x.y;
+        R[k].v[2] = x.z;
+        R[k].v[3] = x.w;
+    }
+    // lane q holds row q of M[chunk][owner]; transpose so that it holds column q
+    Chunk S[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool take = ((k ^ q) & 1) != 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int o = dpp_xor<1>(R[k ^ 1].v[c]);
+            S[k].v[c] = take ? o : R[k].v[c];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool take = ((k ^ q) & 2) != 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int o = dpp_xor<2>(S[k ^ 2].v[c]);
+            R[k].v[c] = take ? o : S[k].v[c];
+        }
+    }
+    na = make_float4(__int_as_float(R[0].v[0]), __int_as_float(R[0].v[1]), __int_as_float(R[0].v[2]),
+                     __int_as_float(R[0].v[3]));
+    nb = make_float4(__int_as_float(R[1].v[0]), __int_as_float(R[1].v[1]), __int_as_float(R[1].v[2]),
+                     __int_as_float(R[1].v[3]));
+    nc = make_float4(__int_as_float(R[2].v[0]), __int_as_float(R[2].v[1]), __int_as_float(R[2].v[2]),
+                     __int_as_float(R[2].v[3]));
+    nd = make_int4(R[3].v[0], R[3].v[1], R[3].v[2], R[3].v[3]);
+}
+
+// node_step3 with the quad-cooperative fetch: the pop is per lane, the fetch is wave-wide,
+// the box tests and stack updates are per lane again.
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void node_step6(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, bool& overflow, bool can_node) {
+    int node = -1;
+    if (can_node) {
+        if (t.node < 0) {  // pop
+            --t.sp;
+            const int e = stk[t.sp * BLOCK + lane];
+            if (e >= 0) {
+                t.node = e;
+            } else {
+                const int v = -e - 1;
+                t.pf = v >> 4;
+                t.pc = v & 15;
+            }
+        }
+        node = t.node;
+    }
+    float4 na, nb, nc;
+    int4 nd;
+    coop_fetch_node(a.nodes, node >= 0 ? node : 0, lane, na, nb, nc, nd);
+    if (node < 0) return;
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = tn0 <= tf0 && nd.z >= 0;
+    const bool h1 = tn1 <= tf1 && nd.w >= 0;
+    const bool l0 = h0 && nd.z > 0, l1 = h1 && nd.w > 0;
+    const bool i0 = h0 && nd.z == 0, i1 = h1 && nd.w == 0;
+    if (l0 && l1) {
+        const bool swap = tn1 < tn0;
+        t.pf = swap ? nd.y : nd.x;
+        t.pc = swap ? nd.w : nd.z;
+        push3<BLOCK, STACK>(t, stk, lane, swap ? leaf_code(nd.x, nd.z) : leaf_code(nd.y, nd.w), overflow);
+    } else if (l0) {
+        t.pf = nd.x;
+        t.pc = nd.z;
+    } else if (l1) {
+        t.pf = nd.y;
+        t.pc = nd.w;
+    }
+    if (i0 && i1) {
+        const bool swap = tn1 < tn0;
+        push3<BLOCK, STACK>(t, stk, lane, swap ? nd.x : nd.y, overflow);
+        t.node = swap ? nd.y : nd.x;
+    } else if (i0) {
+        t.node = nd.x;
+    } else if (i1) {
+        t.node = nd.y;
+    } else {
+        t.node = -1;
+    }
+}
+
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1, int NS = 3>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
@@ -916,7 +1048,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     ++d_nit;
                     d_nl += __popcll(m_node);
                 }
-                if (can_node) {
+                if constexpr (NS == 6) {
+                    node_step6<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, can_node);  // all lanes
+                } else if (can_node) {
                     if constexpr (NS == 5)
                         node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else
@@ -1464,6 +1598,17 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 508: return launch_v3<128, 40, 12, 28, 5, false, 1, 5>(a, cus, s);
         case 509: return launch_v3<64, 32, 12, 28, 5, false, 1, 5>(a, cus, s);
         case 598: return launch_v3<128, 32, 12, 28, 5, true, 1, 5>(a, cus, s);  // instrumented
+        // quad-cooperative node fetch (NS = 6)
+        case 600: return launch_v3<128, 32, 12, 28, 5, false, 1, 6>(a, cus, s);
+        case 601: return launch_v3<128, 32, 12, 28, 5, false, 2, 6>(a, cus, s);
+        case 602: return launch_v3<128, 32, 8, 28, 5, false, 1, 6>(a, cus, s);
+        case 603: return launch_v3<128, 32, 16, 28, 5, false, 1, 6>(a, cus, s);
+        case 604: return launch_v3<128, 24, 12, 28, 5, false, 1, 6>(a, cus, s);
+        case 605: return launch_v3<128, 40, 12, 28, 5, false, 1, 6>(a, cus, s);
+        case 606: return launch_v3<128, 32, 12, 28, 4, false, 1, 6>(a, cus, s);
+        case 607: return launch_v3<128, 32, 12, 28, 6, false, 1, 6>(a, cus, s);
+        case 608: return launch_v3<64, 32, 12, 28, 5, false, 1, 6>(a, cus, s);
+        case 698: return launch_v3<128, 32, 12, 28, 5, true, 1, 6>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
