@@ -949,7 +949,7 @@ __device__ __forceinline__ void node_step6(const TraceArgs& a, const Ray& r, flo
 
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1, int NS = 3>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
-    uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0;
+    uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0, d_pend = 0, d_inact = 0;
     uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
     if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
@@ -1047,6 +1047,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                 if constexpr (DBG) {
                     ++d_nit;
                     d_nl += __popcll(m_node);
+                    d_pend += __popcll(m_leaf);
+                    d_inact += __popcll(__ballot(!active));
                 }
                 if constexpr (NS == 6) {
                     node_step6<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, can_node);  // all lanes
@@ -1095,6 +1097,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             atomicAdd(a.counters + 5, (unsigned long long)c_node);
             atomicAdd(a.counters + 15, (unsigned long long)c_leaf);
             atomicAdd(a.counters + 7, (unsigned long long)c_outer);
+            atomicAdd(a.counters + 6, (unsigned long long)(d_pend << 32 | (d_inact & 0xffffffffull)));
         }
     }
 }

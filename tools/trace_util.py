@@ -28,6 +28,9 @@ print(f"node steps: {nit} wave-iterations, {nl} lane-steps = {nl / q:.1f} per qu
 print(f"leaf steps: {lit} wave-iterations, {ll} lane-steps = {ll / q:.1f} per query, utilisation {ll / (64 * max(lit, 1)):.3f}")
 print(f"idle lanes per inner iteration {idle / max(nit + lit, 1):.1f} of 64")
 print(f"wave-iterations per query: node {nit / q:.3f} leaf {lit / q:.3f} outer {outer / q:.3f}")
+pend, inact = c[6] >> 32, c[6] & 0xffffffff
+print(f"per node iteration: node lanes {nl / nit:.1f}, pending-leaf lanes {pend / nit:.1f}, "
+      f"no-ray lanes {inact / nit:.1f} (approx., 32-bit packed) of 64")
 cn, cl, co = c[5], c[15], c[7]
 tot = cn + cl + co
 print(f"wave cycles (s_memtime): node {cn / tot:.3f}  leaf {cl / tot:.3f}  outer/shade/refill {co / tot:.3f}")
