@@ -91,6 +91,8 @@ struct arx_renderer {
     size_t spill_cap = 0;   // int32 entries
     int32_t stack_need = 0;
     uint8_t* d_stash = nullptr;  // phased-launch ray stash (2 x lanes x 48 B)
+    void* d_dirs = nullptr;      // direction pre-pass (float4 per ray of the largest trace call)
+    uint64_t dirs_cap = 0;
     unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
     unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
     unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
@@ -401,6 +403,7 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_wnodes);
     hipFree(r->d_spill);
     hipFree(r->d_stash);
+    hipFree(r->d_dirs);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
@@ -562,6 +565,15 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.stash_count = r->d_counters + 6;
     a.stash_cap = trace_spill_lanes(r->cus);
     a.pool_from = -1;
+    if (ray_end - ray_begin > r->dirs_cap) {  // direction pre-pass buffer of the refill variants
+        if (r->d_dirs) ARX_HIP(hipFree(r->d_dirs));
+        r->d_dirs = nullptr;
+        r->dirs_cap = 0;
+        ARX_HIP(hipMalloc(&r->d_dirs, (ray_end - ray_begin) * 16));
+        r->dirs_cap = ray_end - ray_begin;
+    }
+    a.dirs_buf = r->d_dirs;
+    a.dirs_cap = r->dirs_cap;
     if (ray_end == ray_begin) return ARX_OK;
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream));

@@ -111,6 +111,12 @@ struct TraceArgs {
     // set by the launcher per phase: source pool (-1 = fresh ray ids) and drain threshold
     int32_t pool_from;   // -1 or 0/1: read states from stash[pool_from]
     int32_t drain_low;   // 0: never drain; else drain a wave once exhausted with < drain_low active lanes
+    // refill options (kernel variants 700+): precomputed directions of rays [ray_begin, ray_end)
+    // as float4(dir, 0), and static per-wave ray ranges instead of the global cursor
+    const void* dirs;
+    int32_t static_ranges;
+    void* dirs_buf;      // capacity for the launcher's direction pre-pass (dirs_cap rays)
+    uint64_t dirs_cap;
 };
 
 }  // namespace arx

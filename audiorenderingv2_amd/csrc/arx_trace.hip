@@ -415,7 +415,12 @@ __device__ __forceinline__ bool wants_query(const TraceArgs& a, const RayState& 
 }
 
 __device__ __forceinline__ void ray_init(const TraceArgs& a, RayState& s, uint64_t rid) {
-    s.dir = ray_direction(a.seed, rid);
+    if (a.dirs) {  // precomputed by dirs_kernel (same function, launcher pre-pass)
+        const float4 d = reinterpret_cast<const float4*>(a.dirs)[rid - a.ray_begin];
+        s.dir = make_float3(d.x, d.y, d.z);
+    } else {
+        s.dir = ray_direction(a.seed, rid);
+    }
     s.pos = make_float3(a.emitter[0], a.emitter[1], a.emitter[2]);
     s.e = a.e0;
     s.dist = 0.0f;
@@ -955,6 +960,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
     const int lane = threadIdx.x;
     const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
+    // static per-wave ranges (a.static_ranges): wave w owns pool entries [w_next, w_end)
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    uint64_t w_next = n * wave_id / n_waves;
+    const uint64_t w_end = n * (wave_id + 1) / n_waves;
     bool draining = false;
     unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
@@ -989,17 +999,24 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
         const unsigned long long need = __ballot(!active);
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
-            const int leader = __ffsll((unsigned long long)need) - 1;
             unsigned long long base = 0;
-            if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
-            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
-            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
-            base = ((unsigned long long)hi << 32) | lo;
+            uint64_t lim = n;
+            if (a.static_ranges) {  // wave-uniform, no atomic on the critical path
+                base = w_next;
+                lim = w_end;
+                w_next += (uint64_t)cnt;
+            } else {
+                const int leader = __ffsll((unsigned long long)need) - 1;
+                if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+                base = ((unsigned long long)hi << 32) | lo;
+            }
             if (!active) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint64_t i = base + rank;
-                if (i < n) {
+                if (i < lim) {
                     if (a.pool_from < 0)
                         ray_init(a, s, a.ray_begin + i);
                     else
@@ -1007,7 +1024,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     active = wants_query(a, s);
                 }
             }
-            if (base + (unsigned long long)cnt >= n) exhausted = true;
+            if (base + (unsigned long long)cnt >= lim) exhausted = true;
         }
         if (active && !trav) {
             ++n_q;
@@ -1430,6 +1447,14 @@ __global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __
     R[k] = r;
 }
 
+// Direction pre-pass of the refill variants: float4(dir, 0) for rays [first, first + count).
+__global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float3 d = ray_direction(seed, first + i);
+    out[i] = make_float4(d.x, d.y, d.z, 0.0f);
+}
+
 __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, float* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -1480,9 +1505,19 @@ int env_int(const char* name, int def) {
 // that stash.  The last phase runs to completion.  Counts live on the device, so the phases
 // are enqueued back to back without host synchronisation; empty phases exit immediately.
 template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false, int LV = 1,
-          int NS = 3>
+          int NS = 3, int REFILL = 0>
 hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     TraceArgs a = args;
+    // REFILL bit 0: directions from a pre-pass; bit 1: static per-wave ranges
+    a.dirs = nullptr;
+    a.static_ranges = (REFILL & 2) ? 1 : 0;
+    const uint64_t n_rays = a.ray_end - a.ray_begin;
+    if ((REFILL & 1) && a.dirs_buf && n_rays <= a.dirs_cap && n_rays > 0) {
+        const uint64_t g = (n_rays + 255) / 256;
+        hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)g), dim3(256), 0, s, a.seed, a.ray_begin, n_rays,
+                           reinterpret_cast<float4*>(a.dirs_buf));
+        a.dirs = a.dirs_buf;
+    }
     auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
     const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 1)) : 1;
@@ -1616,6 +1651,17 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 607: return launch_v3<128, 32, 12, 28, 6, false, 1, 6>(a, cus, s);
         case 608: return launch_v3<64, 32, 12, 28, 5, false, 1, 6>(a, cus, s);
         case 698: return launch_v3<128, 32, 12, 28, 5, true, 1, 6>(a, cus, s);  // instrumented
+        // refill: 701 pre-pass directions, 702 static ranges, 703 both; then THRESH retunes
+        case 701: return launch_v3<128, 32, 12, 28, 5, false, 1, 3, 1>(a, cus, s);
+        case 702: return launch_v3<128, 32, 12, 28, 5, false, 1, 3, 2>(a, cus, s);
+        case 703: return launch_v3<128, 32, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 704: return launch_v3<128, 24, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 705: return launch_v3<128, 16, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 706: return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 707: return launch_v3<128, 8, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 708: return launch_v3<128, 40, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 709: return launch_v3<128, 24, 8, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 798: return launch_v3<128, 32, 12, 28, 5, true, 1, 3, 3>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
