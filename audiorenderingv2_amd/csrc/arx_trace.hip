@@ -1345,6 +1345,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_w(TraceArgs a) {
     const int lane = threadIdx.x;
     const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
     const uint64_t n = a.ray_end - a.ray_begin;
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    uint64_t w_next = n * wave_id / n_waves;
+    const uint64_t w_end = n * (wave_id + 1) / n_waves;
     unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
     bool overflow = false;
@@ -1372,22 +1376,29 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_w(TraceArgs a) {
         const unsigned long long need = __ballot(!active);
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
-            const int leader = __ffsll((unsigned long long)need) - 1;
             unsigned long long base = 0;
-            if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
-            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
-            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
-            base = ((unsigned long long)hi << 32) | lo;
+            uint64_t lim = n;
+            if (a.static_ranges) {
+                base = w_next;
+                lim = w_end;
+                w_next += (uint64_t)cnt;
+            } else {
+                const int leader = __ffsll((unsigned long long)need) - 1;
+                if ((lane & 63) == leader) base = atomicAdd(cursor, (unsigned long long)cnt);
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)base, leader);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(base >> 32), leader);
+                base = ((unsigned long long)hi << 32) | lo;
+            }
             if (!active) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint64_t i = base + rank;
-                if (i < n) {
+                if (i < lim) {
                     ray_init(a, s, a.ray_begin + i);
                     active = wants_query(a, s);
                 }
             }
-            if (base + (unsigned long long)cnt >= n) exhausted = true;
+            if (base + (unsigned long long)cnt >= lim) exhausted = true;
         }
         if (active && !trav) {
             ++n_q;
@@ -1539,9 +1550,18 @@ hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     }
     return hipSuccess;
 }
-template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW>
+template <int W, int BLOCK, int S, int THRESH, int LEAF_THRESH, int MINW, int REFILL = 0>
 hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
     if (!a.wnodes) return hipErrorInvalidValue;
+    a.dirs = nullptr;
+    a.static_ranges = (REFILL & 2) ? 1 : 0;
+    const uint64_t n_rays = a.ray_end - a.ray_begin;
+    if ((REFILL & 1) && a.dirs_buf && n_rays <= a.dirs_cap && n_rays > 0) {
+        const uint64_t g = (n_rays + 255) / 256;
+        hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)g), dim3(256), 0, s, a.seed, a.ray_begin, n_rays,
+                           reinterpret_cast<float4*>(a.dirs_buf));
+        a.dirs = a.dirs_buf;
+    }
     hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // ray cursor
     if (e != hipSuccess) return e;
     auto k = trace_kernel_w<W, BLOCK, S, THRESH, LEAF_THRESH, MINW>;
@@ -1562,7 +1582,7 @@ int trace_width() {
     const int v = trace_variant();
     if (v >= 300 && v < 310) return 4;
     if (v >= 310 && v < 320) return 8;
-    if (v >= 320 && v < 340) return kWideQ4;
+    if ((v >= 320 && v < 340) || (v >= 720 && v < 730)) return kWideQ4;
     return 2;
 }
 
@@ -1662,6 +1682,21 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 708: return launch_v3<128, 40, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
         case 709: return launch_v3<128, 24, 8, 28, 5, false, 1, 3, 3>(a, cus, s);
         case 798: return launch_v3<128, 32, 12, 28, 5, true, 1, 3, 3>(a, cus, s);  // instrumented
+        case 710: return launch_v3<128, 12, 8, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 711: return launch_v3<128, 12, 16, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 712: return launch_v3<128, 10, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 713: return launch_v3<128, 14, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 714: return launch_v3<128, 12, 12, 28, 5, false, 2, 3, 3>(a, cus, s);
+        case 715: return launch_v3<128, 12, 6, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 716: return launch_v3<64, 12, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+        case 717: return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 1>(a, cus, s);
+        // quantized 4-wide + refill
+        case 720: return launch_w<kWideQ4, 128, 24, 12, 12, 5, 3>(a, cus, s);
+        case 721: return launch_w<kWideQ4, 128, 24, 16, 12, 5, 3>(a, cus, s);
+        case 722: return launch_w<kWideQ4, 128, 24, 8, 12, 5, 3>(a, cus, s);
+        case 723: return launch_w<kWideQ4, 128, 28, 12, 12, 5, 3>(a, cus, s);
+        case 724: return launch_w<kWideQ4, 128, 24, 12, 8, 5, 3>(a, cus, s);
+        case 725: return launch_w<kWideQ4, 128, 24, 12, 16, 5, 3>(a, cus, s);
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
