@@ -642,8 +642,11 @@ __device__ __forceinline__ void push3(Trav3& t, int* __restrict__ stk, int lane,
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 // One node step for a lane with no pending leaf and work left (node >= 0 or sp > 0).
-template <int BLOCK, int STACK>
+// PK: the 12 slab FMAs as 6 v_pk_fma_f32 (same IEEE result per element).
+template <int BLOCK, int STACK, bool PK = false>
 __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
                                            int* __restrict__ stk, int lane, bool& overflow) {
     if (t.node < 0) {  // pop
@@ -664,14 +667,28 @@ __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, flo
     const float4 nc = np[2];
     const int4 nd = *reinterpret_cast<const int4*>(np + 3);
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
-    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
-    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
-    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    float x00, x01, y00, y01, z00, z01, x10, x11, y10, y11, z10, z11;
+    if constexpr (PK) {
+        const f2v ix2 = {ix, ix}, iy2 = {iy, iy}, iz2 = {iz, iz};
+        const f2v ox2 = {-oix, -oix}, oy2 = {-oiy, -oiy}, oz2 = {-oiz, -oiz};
+        const f2v X0 = __builtin_elementwise_fma((f2v){na.x, na.y}, ix2, ox2);
+        const f2v Y0 = __builtin_elementwise_fma((f2v){na.z, na.w}, iy2, oy2);
+        const f2v Z0 = __builtin_elementwise_fma((f2v){nc.x, nc.y}, iz2, oz2);
+        const f2v X1 = __builtin_elementwise_fma((f2v){nb.x, nb.y}, ix2, ox2);
+        const f2v Y1 = __builtin_elementwise_fma((f2v){nb.z, nb.w}, iy2, oy2);
+        const f2v Z1 = __builtin_elementwise_fma((f2v){nc.z, nc.w}, iz2, oz2);
+        x00 = X0.x; x01 = X0.y; y00 = Y0.x; y01 = Y0.y; z00 = Z0.x; z01 = Z0.y;
+        x10 = X1.x; x11 = X1.y; y10 = Y1.x; y11 = Y1.y; z10 = Z1.x; z11 = Z1.y;
+    } else {
+        x00 = __builtin_fmaf(na.x, ix, -oix); x01 = __builtin_fmaf(na.y, ix, -oix);
+        y00 = __builtin_fmaf(na.z, iy, -oiy); y01 = __builtin_fmaf(na.w, iy, -oiy);
+        z00 = __builtin_fmaf(nc.x, iz, -oiz); z01 = __builtin_fmaf(nc.y, iz, -oiz);
+        x10 = __builtin_fmaf(nb.x, ix, -oix); x11 = __builtin_fmaf(nb.y, ix, -oix);
+        y10 = __builtin_fmaf(nb.z, iy, -oiy); y11 = __builtin_fmaf(nb.w, iy, -oiy);
+        z10 = __builtin_fmaf(nc.z, iz, -oiz); z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    }
     const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
     const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
-    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
-    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
-    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
     const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
     const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
     const bool h0 = tn0 <= tf0 && nd.z >= 0;
@@ -1072,6 +1089,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                 } else if (can_node) {
                     if constexpr (NS == 5)
                         node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    else if constexpr (NS == 7)
+                        node_step3<BLOCK, STACK, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else
                         node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                 }
@@ -1697,6 +1716,13 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 723: return launch_w<kWideQ4, 128, 28, 12, 12, 5, 3>(a, cus, s);
         case 724: return launch_w<kWideQ4, 128, 24, 12, 8, 5, 3>(a, cus, s);
         case 725: return launch_w<kWideQ4, 128, 24, 12, 16, 5, 3>(a, cus, s);
+        // packed slab FMAs (NS = 7) on the 706 configuration
+        case 730: return launch_v3<128, 12, 12, 28, 5, false, 1, 7, 3>(a, cus, s);
+        case 731: return launch_v3<128, 14, 12, 28, 5, false, 1, 7, 3>(a, cus, s);
+        case 732: return launch_v3<128, 12, 12, 28, 5, false, 2, 7, 3>(a, cus, s);
+        case 733: return launch_v3<128, 32, 12, 28, 5, false, 1, 7, 0>(a, cus, s);
+        case 739: return launch_v3<128, 12, 12, 28, 5, true, 1, 7, 3>(a, cus, s);  // instrumented
+        case 799: return launch_v3<128, 12, 12, 28, 5, true, 1, 3, 3>(a, cus, s);  // instrumented 706
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
