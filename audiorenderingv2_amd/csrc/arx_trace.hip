@@ -969,12 +969,26 @@ __device__ __forceinline__ void node_step6(const TraceArgs& a, const Ray& r, flo
     }
 }
 
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1, int NS = 3>
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, bool DBG = false, int LV = 1, int NS = 3,
+          int MIG = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t d_outer = 0, d_nit = 0, d_nl = 0, d_lit = 0, d_ll = 0, d_sh = 0, d_idle = 0, d_pend = 0, d_inact = 0;
     uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
     if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
+    // MIG > 0: block-level ray migration (see migrate comment below); LDS queue of parked rays
+    constexpr int MQ = MIG > 0 ? 64 : 1;
+    __shared__ float4 mq_a[MQ], mq_b[MQ];
+    __shared__ int mq_d[MQ];
+    __shared__ int mq_lock, mq_count, mq_live;
+    if constexpr (MIG > 0) {
+        if (threadIdx.x == 0) {
+            mq_lock = 0;
+            mq_count = 0;
+            mq_live = BLOCK / 64;
+        }
+        __syncthreads();
+    }
     const int lane = threadIdx.x;
     const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
     // static per-wave ranges (a.static_ranges): wave w owns pool entries [w_next, w_end)
@@ -1042,6 +1056,74 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                 }
             }
             if (base + (unsigned long long)cnt >= lim) exhausted = true;
+        }
+        if constexpr (MIG > 0) {
+            // Block-level migration once this wave's range is exhausted.  Under an LDS lock:
+            //  * a sparse wave (<= MIG rays, all at a query boundary) parks its rays in the block
+            //    queue and exits -- unless it is the last live wave of the block;
+            //  * a wave with empty lanes pulls parked rays;
+            //  * a wave with no rays exits only when the queue is empty.
+            // The last live wave never parks, so parked rays are always picked up; no wave ever
+            // waits for another (the lock is held for a few LDS operations only).
+            if (exhausted) {
+                const unsigned long long act = __ballot(active);
+                const unsigned long long bnd = __ballot(active && !trav);
+                const int n_act = __popcll(act);
+                const int wl = lane & 63;
+                if (wl == 0) {
+                    while (atomicCAS(&mq_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const int qcnt = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mq_count, __ATOMIC_RELAXED,
+                                                                                  __HIP_MEMORY_SCOPE_WORKGROUP));
+                const int live = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&mq_live, __ATOMIC_RELAXED,
+                                                                                  __HIP_MEMORY_SCOPE_WORKGROUP));
+                bool leave = false;
+                int new_cnt = qcnt, new_live = live;
+                if (n_act > 0 && act == bnd && n_act <= MIG && live > 1 && qcnt + n_act <= MQ) {
+                    if (active) {
+                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                        const int slot = qcnt + (int)rank;
+                        mq_a[slot] = make_float4(s.pos.x, s.pos.y, s.pos.z, s.e);
+                        mq_b[slot] = make_float4(s.dir.x, s.dir.y, s.dir.z, s.dist);
+                        mq_d[slot] = s.depth;
+                        active = false;
+                    }
+                    new_cnt = qcnt + n_act;
+                    new_live = live - 1;
+                    leave = true;
+                } else if (n_act < 64 && qcnt > 0) {
+                    const int take = min(qcnt, 64 - n_act);
+                    if (!active) {
+                        const unsigned long long idle = ~act;
+                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                        if ((int)rank < take) {
+                            const int slot = qcnt - 1 - (int)rank;
+                            const float4 qa = mq_a[slot], qb = mq_b[slot];
+                            s.pos = make_float3(qa.x, qa.y, qa.z);
+                            s.e = qa.w;
+                            s.dir = make_float3(qb.x, qb.y, qb.z);
+                            s.dist = qb.w;
+                            s.depth = mq_d[slot];
+                            active = true;  // parked at a query boundary that wanted a query
+                        }
+                    }
+                    new_cnt = qcnt - take;
+                } else if (n_act == 0 && qcnt == 0) {
+                    new_live = live - 1;
+                    leave = true;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (wl == 0) {
+                    __hip_atomic_store(&mq_count, new_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&mq_live, new_live, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    atomicExch(&mq_lock, 0);
+                }
+                if (leave) break;
+            }
         }
         if (active && !trav) {
             ++n_q;
@@ -1535,7 +1617,7 @@ int env_int(const char* name, int def) {
 // that stash.  The last phase runs to completion.  Counts live on the device, so the phases
 // are enqueued back to back without host synchronisation; empty phases exit immediately.
 template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int MINW = 1, bool DBG = false, int LV = 1,
-          int NS = 3, int REFILL = 0>
+          int NS = 3, int REFILL = 0, int MIG = 0>
 hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     TraceArgs a = args;
     // REFILL bit 0: directions from a pre-pass; bit 1: static per-wave ranges
@@ -1548,7 +1630,7 @@ hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
                            reinterpret_cast<float4*>(a.dirs_buf));
         a.dirs = a.dirs_buf;
     }
-    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS>;
+    auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS, MIG>;
     const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
     const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 1)) : 1;
     const int low = env_int("ARX_DRAIN_LOW", 32);
@@ -1723,6 +1805,17 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 733: return launch_v3<128, 32, 12, 28, 5, false, 1, 7, 0>(a, cus, s);
         case 739: return launch_v3<128, 12, 12, 28, 5, true, 1, 7, 3>(a, cus, s);  // instrumented
         case 799: return launch_v3<128, 12, 12, 28, 5, true, 1, 3, 3>(a, cus, s);  // instrumented 706
+        // block-level ray migration (MIG = park threshold), larger blocks
+        case 800: return launch_v3<256, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 801: return launch_v3<512, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 802: return launch_v3<640, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 803: return launch_v3<512, 12, 12, 28, 5, false, 1, 3, 3, 32>(a, cus, s);
+        case 804: return launch_v3<512, 12, 12, 28, 5, false, 1, 3, 3, 16>(a, cus, s);
+        case 805: return launch_v3<640, 12, 12, 28, 5, false, 1, 3, 3, 40>(a, cus, s);
+        case 806: return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 807: return launch_v3<512, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
+        case 808: return launch_v3<640, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
+        case 898: return launch_v3<640, 12, 12, 28, 5, true, 1, 3, 3, 24>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
