@@ -1065,10 +1065,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             //  * a wave with no rays exits only when the queue is empty.
             // The last live wave never parks, so parked rays are always picked up; no wave ever
             // waits for another (the lock is held for a few LDS operations only).
-            if (exhausted) {
-                const unsigned long long act = __ballot(active);
-                const unsigned long long bnd = __ballot(active && !trav);
-                const int n_act = __popcll(act);
+            const unsigned long long act = __ballot(active);
+            const unsigned long long bnd = __ballot(active && !trav);
+            const int n_act = __popcll(act);
+            const int peek = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&mq_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            // the lock is only worth taking to park (sparse wave at a boundary), to pull (queue
+            // non-empty) or to leave (no rays); the decision is re-checked under the lock
+            const bool want = (n_act > 0 && act == bnd && n_act <= MIG) || (n_act < 64 && peek > 0) || n_act == 0;
+            if (exhausted && want) {
                 const int wl = lane & 63;
                 if (wl == 0) {
                     while (atomicCAS(&mq_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
@@ -1583,7 +1588,7 @@ int trace_block_size() { return kBlock; }
 namespace {
 // Kernel variants for A/B measurement (ARX_TRACE_KERNEL, read per launch); all are
 // bit-identical in results.  Default = the fastest measured on MI355X.
-constexpr int kDefaultVariant = 0;  // 0 = v3<128, 32, 12, stack by tree depth, 5 waves/SIMD>
+constexpr int kDefaultVariant = 0;  // 0 = v3<128, 12, 12, stack by tree depth, 5 waves/SIMD, refill 3>
 
 template <typename K>
 int persistent_grid(K kernel, int block, uint64_t n_rays, int cus) {
@@ -1815,7 +1820,15 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 806: return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
         case 807: return launch_v3<512, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
         case 808: return launch_v3<640, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
-        case 898: return launch_v3<640, 12, 12, 28, 5, true, 1, 3, 3, 24>(a, cus, s);  // instrumented
+        case 810: return launch_v3<320, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 811: return launch_v3<320, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
+        case 812: return launch_v3<384, 12, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 813: return launch_v3<384, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
+        case 814: return launch_v3<256, 12, 12, 28, 5, false, 1, 3, 3, 0>(a, cus, s);
+        case 815: return launch_v3<320, 12, 12, 28, 5, false, 1, 3, 3, 32>(a, cus, s);
+        case 816: return launch_v3<320, 12, 12, 28, 5, false, 1, 3, 3, 16>(a, cus, s);
+        case 817: return launch_v3<320, 16, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
+        case 898: return launch_v3<320, 12, 12, 28, 5, true, 1, 3, 3, 24>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
@@ -1840,10 +1853,10 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 327: return launch_w<kWideQ4, 128, 24, 32, 24, 5>(a, cus, s);
         case 328: return launch_w<kWideQ4, 256, 24, 64, 12, 5>(a, cus, s);
         case 329: return launch_w<kWideQ4, 128, 28, 32, 12, 5>(a, cus, s);
-        default:
-            if (a.bvh_depth < 28) return launch_v3<128, 32, 12, 28, 5>(a, cus, s);
-            if (a.bvh_depth < 40) return launch_v3<128, 32, 12, 40, 5>(a, cus, s);
-            return launch_v3<128, 32, 12, kMaxStackDepth, 5>(a, cus, s);
+        default:  // = 706: static per-wave ray ranges, direction pre-pass, refill at 12 idle lanes
+            if (a.bvh_depth < 28) return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
+            if (a.bvh_depth < 40) return launch_v3<128, 12, 12, 40, 5, false, 1, 3, 3>(a, cus, s);
+            return launch_v3<128, 12, 12, kMaxStackDepth, 5, false, 1, 3, 3>(a, cus, s);
     }
 }
 
