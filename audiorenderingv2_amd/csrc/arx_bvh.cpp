@@ -510,11 +510,17 @@ bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes
 }
 
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why) {
+    return validate_bvh_range(nodes, 0, n_nodes, n_nodes, n_tris, why);
+}
+
+bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                        const char** why) {
     // Every inner child must have a larger index than its parent (the builder emits nodes in
     // pre-order): that makes the graph acyclic, so traversal always terminates.
-    for (size_t i = 0; i < n_nodes; ++i) {
+    for (size_t k = 0; k < n_nodes; ++k) {
+        const size_t i = first + k;
         for (int c = 0; c < 2; ++c) {
-            const int32_t ref = nodes[i].d[c], count = nodes[i].d[2 + c];
+            const int32_t ref = nodes[k].d[c], count = nodes[k].d[2 + c];
             if (count < 0) continue;
             if (count > 0) {
                 if (ref < 0 || (size_t)ref + (size_t)count > n_tris) {
@@ -525,7 +531,7 @@ bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const cha
                     *why = "leaf larger than 15 triangles or beyond 2^27 (degenerate scene)";
                     return false;
                 }
-            } else if (ref <= (int64_t)i || (size_t)ref >= n_nodes) {
+            } else if (ref <= (int64_t)i || (size_t)ref >= total_nodes) {
                 *why = "inner child index not after its parent";
                 return false;
             }

@@ -42,6 +42,10 @@ BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
 ChildRef empty_child();
 // Structural check of a device-ready node array (acyclic, references in range).
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why);
+// Same check for nodes [first, first + n_nodes) of an array of total_nodes (`nodes` points at node
+// `first`), so a listener move re-validates only the receiver sub-tree and the top node.
+bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
+                        const char** why);
 
 // Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
 struct WideBuild {

@@ -263,13 +263,14 @@ arx_status ensure_device_scene(arx_renderer* r) {
     if (full || r->recv_dirty) {
         BvhNode top = make_node(r->scene.root, r->recv.root);
         {
-            std::vector<BvhNode> all;
-            all.reserve(n_nodes);
-            all.push_back(top);
-            all.insert(all.end(), r->scene.nodes.begin(), r->scene.nodes.end());
-            all.insert(all.end(), r->recv.nodes.begin(), r->recv.nodes.end());
+            // structure check (acyclic, in range): the scene part when it changed, the receiver
+            // part and the top node on every listener move
             const char* why = "";
-            if (!validate_bvh(all.data(), all.size(), n_tris, &why))
+            if (full && !validate_bvh_range(r->scene.nodes.data(), 1, r->scene.nodes.size(), n_nodes, n_tris, &why))
+                return fail(ARX_ERR_INTERNAL, "BVH validation failed (scene): %s", why);
+            if (!validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(), n_nodes,
+                                    n_tris, &why) ||
+                !validate_bvh_range(&top, 0, 1, n_nodes, n_tris, &why))
                 return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
         }
         ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
