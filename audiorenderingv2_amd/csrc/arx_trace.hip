@@ -1181,6 +1181,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     else
                         node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                 }
+                if constexpr (NS == 8) {  // a second step for lanes that can go on (no loop control)
+                    if (can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0))
+                        node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                }
                 if constexpr (DBG) {
                     const uint64_t now = __builtin_amdgcn_s_memtime();
                     c_node += now - c_mark;
@@ -1829,6 +1833,12 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 816: return launch_v3<320, 12, 12, 28, 5, false, 1, 3, 3, 16>(a, cus, s);
         case 817: return launch_v3<320, 16, 12, 28, 5, false, 1, 3, 3, 24>(a, cus, s);
         case 898: return launch_v3<320, 12, 12, 28, 5, true, 1, 3, 3, 24>(a, cus, s);  // instrumented
+        // two node steps per inner iteration (NS = 8)
+        case 740: return launch_v3<128, 12, 12, 28, 5, false, 1, 8, 3>(a, cus, s);
+        case 741: return launch_v3<128, 16, 12, 28, 5, false, 1, 8, 3>(a, cus, s);
+        case 742: return launch_v3<128, 12, 16, 28, 5, false, 1, 8, 3>(a, cus, s);
+        case 743: return launch_v3<128, 12, 8, 28, 5, false, 1, 8, 3>(a, cus, s);
+        case 749: return launch_v3<128, 12, 12, 28, 5, true, 1, 8, 3>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
