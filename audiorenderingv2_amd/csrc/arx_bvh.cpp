@@ -540,4 +540,17 @@ bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size
     return true;
 }
 
+void code_nodes(const BvhNode* in, size_t n, BvhNode* out) {
+    for (size_t i = 0; i < n; ++i) {
+        BvhNode o = in[i];
+        for (int c = 0; c < 2; ++c) {
+            const int32_t ref = in[i].d[c], count = in[i].d[2 + c];
+            o.d[c] = count < 0 ? -1 : count == 0 ? ref : ~(ref * 16 + count);
+        }
+        o.d[2] = 0;
+        o.d[3] = 0;
+        out[i] = o;
+    }
+}
+
 }  // namespace arx

@@ -46,6 +46,11 @@ bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const cha
 // `first`), so a listener move re-validates only the receiver sub-tree and the top node.
 bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
                         const char** why);
+// Coded copy of validated nodes for the coded node step: d = (code0, code1, 0, 0) with
+// code = inner node index (>= 0), ~(first*16 + count) for a leaf (< 0; the traversal-stack
+// entry format), or -1 for an empty child (a leaf of 0 triangles, i.e. a no-op if its
+// inverted box ever passes the slab test).  Boxes are unchanged.
+void code_nodes(const BvhNode* in, size_t n, BvhNode* out);
 
 // Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
 struct WideBuild {

@@ -79,6 +79,7 @@ struct arx_renderer {
 
     // device
     BvhNode* d_nodes = nullptr;
+    BvhNode* d_cnodes = nullptr;  // coded copy (code_nodes), same indices
     size_t nodes_cap = 0;
     TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
@@ -246,9 +247,12 @@ arx_status ensure_device_scene(arx_renderer* r) {
     bool full = r->scene_dirty;
     if (n_nodes > r->nodes_cap) {
         if (r->d_nodes) ARX_HIP(hipFree(r->d_nodes));
+        if (r->d_cnodes) ARX_HIP(hipFree(r->d_cnodes));
         r->d_nodes = nullptr;
+        r->d_cnodes = nullptr;
         size_t cap = n_nodes + 1024;
         ARX_HIP(hipMalloc(&r->d_nodes, cap * sizeof(BvhNode)));
+        ARX_HIP(hipMalloc(&r->d_cnodes, cap * sizeof(BvhNode)));
         r->nodes_cap = cap;
         full = true;
     }
@@ -273,16 +277,30 @@ arx_status ensure_device_scene(arx_renderer* r) {
                 !validate_bvh_range(&top, 0, 1, n_nodes, n_tris, &why))
                 return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
         }
+        // coded copies of the parts being uploaded (kept in host vectors that live until the sync)
+        BvhNode ctop;
+        code_nodes(&top, 1, &ctop);
+        std::vector<BvhNode> cscene, crecv(r->recv.nodes.size());
+        code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
         ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-        if (full && !r->scene.nodes.empty())
+        ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+        if (full && !r->scene.nodes.empty()) {
+            cscene.resize(r->scene.nodes.size());
+            code_nodes(r->scene.nodes.data(), r->scene.nodes.size(), cscene.data());
             ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(), r->scene.nodes.size() * sizeof(BvhNode),
                                    hipMemcpyHostToDevice, r->stream));
+            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
+                                   hipMemcpyHostToDevice, r->stream));
+        }
         if (full && !r->scene.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
                                    hipMemcpyHostToDevice, r->stream));
-        if (!r->recv.nodes.empty())
+        if (!r->recv.nodes.empty()) {
             ARX_HIP(hipMemcpyAsync(r->d_nodes + 1 + r->scene.nodes.size(), r->recv.nodes.data(),
                                    r->recv.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
+                                   crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+        }
         if (!r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
                                    r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
@@ -400,6 +418,7 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_live_in);
     hipFree(r->d_live_out);
     hipFree(r->d_nodes);
+    hipFree(r->d_cnodes);
     hipFree(r->d_tris);
     hipFree(r->d_wnodes);
     hipFree(r->d_spill);
@@ -529,6 +548,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     TraceArgs a;
     std::memset(&a, 0, sizeof(a));
     a.nodes = r->d_nodes;
+    a.cnodes = r->d_cnodes;
     a.tris = r->d_tris;
     a.hist = r->hist();
     a.counters = r->d_counters;

@@ -117,6 +117,8 @@ struct TraceArgs {
     int32_t static_ranges;
     void* dirs_buf;      // capacity for the launcher's direction pre-pass (dirs_cap rays)
     uint64_t dirs_cap;
+    // coded copy of `nodes` (code_nodes, arx_bvh.hpp): d = (code0, code1, 0, 0)
+    const BvhNode* cnodes;
 };
 
 }  // namespace arx

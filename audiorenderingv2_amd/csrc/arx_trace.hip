@@ -721,6 +721,53 @@ __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, flo
     }
 }
 
+// Coded node step (nodes from TraceArgs::cnodes, code_nodes in arx_bvh.hpp): a child word is
+// already a stack entry (inner >= 0, leaf < 0, empty = -1 = a 0-triangle leaf), so the step
+// is "hit or not" per child and one nearest-first choice: the nearer hit child is next (a
+// leaf becomes the pending leaf), the farther one is pushed.  (A v_med3 clamp of the z slab
+// looks cheaper but accepts every box behind the ray / beyond the hit that is entered through
+// a z face with tn == tf: 4x the leaf tests.)  Requires t.pc == 0.
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, bool& overflow) {
+    if (t.node < 0) {  // pop
+        --t.sp;
+        const int e = stk[t.sp * BLOCK + lane];
+        if (e < 0) {
+            const int v = ~e;
+            t.pf = v >> 4;
+            t.pc = v & 15;
+            return;
+        }
+        t.node = e;
+    }
+    const float4* np = reinterpret_cast<const float4*>(a.cnodes + t.node);
+    const float4 na = np[0];
+    const float4 nb = np[1];
+    const float4 nc = np[2];
+    const int2 nd = *reinterpret_cast<const int2*>(np + 3);
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+    const bool near1 = h1 && (!h0 || tn1 < tn0);
+    const int next = (h0 || h1) ? (near1 ? nd.y : nd.x) : -1;
+    if (h0 && h1) push3<BLOCK, STACK>(t, stk, lane, near1 ? nd.x : nd.y, overflow);
+    // next >= 0: visit it; next < 0: a leaf (or -1: nothing) becomes the pending leaf, pop after
+    const int v = ~next;
+    t.node = next < 0 ? -1 : next;
+    t.pf = v >> 4;                 // don't care while pc == 0
+    t.pc = next < 0 ? (v & 15) : 0;
+}
+
 // DBG: wave-level utilisation counters in counters[8..15] (variant 98): outer iterations,
 // node-step iterations, lanes in node steps, leaf-step iterations, lanes in leaf steps,
 // lanes shading, lanes idle (active, query done) at node/leaf iterations.
@@ -1174,16 +1221,35 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                 if constexpr (NS == 6) {
                     node_step6<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, can_node);  // all lanes
                 } else if (can_node) {
-                    if constexpr (NS == 5)
+                    if constexpr (NS >= 20)
+                        node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    else if constexpr (NS == 5)
                         node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else if constexpr (NS == 7)
                         node_step3<BLOCK, STACK, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else
                         node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                 }
-                if constexpr (NS == 8) {  // a second step for lanes that can go on (no loop control)
-                    if (can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0))
-                        node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                if constexpr (NS >= 20) {  // coded node step + NS - 20 extra steps
+#pragma unroll
+                    for (int k = 0; k < NS - 20; ++k) {
+                        if (can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0))
+                            node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    }
+                } else if constexpr (NS >= 8) {
+                    // Extra node steps for lanes that can go on, without the loop control above:
+                    // NS 8/9/10 = 1/2/3 extra steps; NS 11/12 = up to 3 while >= 24/16 lanes can;
+                    // NS 13/14 = 5/7 extra; NS 15/16 = up to 7 while >= 24/32; NS 17 = up to 15 while >= 24.
+                    constexpr int kExtra = NS <= 10 ? NS - 7 : NS <= 12 ? 3 : NS == 13 ? 5 : NS <= 16 ? 7 : 15;
+                    constexpr int kMinLanes = (NS == 11 || NS == 15 || NS == 17) ? 24 : NS == 12 ? 16 : NS == 16 ? 32 : 0;
+#pragma unroll
+                    for (int k = 0; k < kExtra; ++k) {
+                        const bool go = can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0);
+                        if constexpr (kMinLanes > 0) {
+                            if (k > 0 && __popcll(__ballot(go)) < kMinLanes) break;
+                        }
+                        if (go) node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    }
                 }
                 if constexpr (DBG) {
                     const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -1838,6 +1904,29 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 741: return launch_v3<128, 16, 12, 28, 5, false, 1, 8, 3>(a, cus, s);
         case 742: return launch_v3<128, 12, 16, 28, 5, false, 1, 8, 3>(a, cus, s);
         case 743: return launch_v3<128, 12, 8, 28, 5, false, 1, 8, 3>(a, cus, s);
+        case 744: return launch_v3<128, 12, 12, 28, 5, false, 1, 9, 3>(a, cus, s);
+        case 745: return launch_v3<128, 12, 12, 28, 5, false, 1, 10, 3>(a, cus, s);
+        case 746: return launch_v3<128, 12, 12, 28, 5, false, 1, 11, 3>(a, cus, s);
+        case 747: return launch_v3<128, 12, 12, 28, 5, false, 1, 12, 3>(a, cus, s);
+        case 748: return launch_v3<128, 16, 16, 28, 5, false, 1, 9, 3>(a, cus, s);
+        case 750: return launch_v3<128, 12, 12, 28, 5, false, 1, 13, 3>(a, cus, s);
+        case 751: return launch_v3<128, 12, 12, 28, 5, false, 1, 14, 3>(a, cus, s);
+        case 752: return launch_v3<128, 12, 12, 28, 5, false, 1, 15, 3>(a, cus, s);
+        case 753: return launch_v3<128, 12, 12, 28, 5, false, 1, 16, 3>(a, cus, s);
+        case 754: return launch_v3<128, 12, 12, 28, 5, false, 1, 17, 3>(a, cus, s);
+        case 755: return launch_v3<128, 12, 16, 28, 5, false, 1, 10, 3>(a, cus, s);
+        case 756: return launch_v3<128, 12, 8, 28, 5, false, 1, 10, 3>(a, cus, s);
+        case 757: return launch_v3<128, 8, 12, 28, 5, false, 1, 10, 3>(a, cus, s);
+        case 758: return launch_v3<128, 16, 12, 28, 5, false, 1, 10, 3>(a, cus, s);
+        case 759: return launch_v3<128, 12, 12, 28, 5, true, 1, 10, 3>(a, cus, s);  // instrumented
+        // coded nodes (node_step7) + extra steps
+        case 760: return launch_v3<128, 12, 12, 28, 5, false, 1, 20, 3>(a, cus, s);
+        case 761: return launch_v3<128, 12, 12, 28, 5, false, 1, 21, 3>(a, cus, s);
+        case 763: return launch_v3<128, 12, 12, 28, 5, false, 1, 23, 3>(a, cus, s);
+        case 765: return launch_v3<128, 12, 12, 28, 5, false, 1, 25, 3>(a, cus, s);
+        case 767: return launch_v3<128, 12, 12, 28, 5, false, 1, 27, 3>(a, cus, s);
+        case 768: return launch_v3<128, 12, 16, 28, 5, false, 1, 27, 3>(a, cus, s);
+        case 769: return launch_v3<128, 12, 12, 28, 5, true, 1, 27, 3>(a, cus, s);  // instrumented
         case 749: return launch_v3<128, 12, 12, 28, 5, true, 1, 8, 3>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
