@@ -315,6 +315,17 @@ arx_status ensure_device_scene(arx_renderer* r) {
     r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
     r->stats.n_nodes = (int64_t)n_nodes;
     r->stats.bvh_depth = 1 + std::max(r->scene.depth, r->recv.depth);
+    if (trace_width() <= 2) {
+        // binary kernels with a short LDS stack spill deeper entries to a per-lane column
+        const size_t need = (size_t)(r->stats.bvh_depth + 1) * trace_spill_lanes(r->cus);
+        if (need > r->spill_cap) {
+            if (r->d_spill) ARX_HIP(hipFree(r->d_spill));
+            r->d_spill = nullptr;
+            r->spill_cap = 0;
+            ARX_HIP(hipMalloc(&r->d_spill, need * sizeof(int32_t)));
+            r->spill_cap = need;
+        }
+    }
     return ARX_OK;
 }
 

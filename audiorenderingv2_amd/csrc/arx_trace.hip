@@ -721,18 +721,54 @@ __device__ __forceinline__ void node_step3(const TraceArgs& a, const Ray& r, flo
     }
 }
 
+// Traversal stack of S entries per lane in LDS; deeper entries spill to a per-lane global
+// column (a.spill[(sp - S) * a.spill_lanes + gid], sized on the host for the tree).
+template <int BLOCK, int S>
+__device__ __forceinline__ void pushw(const TraceArgs& a, Trav3& t, int* __restrict__ stk, int lane, uint32_t gid, int v,
+                                      bool& overflow) {
+    if (t.sp < S) {
+        stk[t.sp * BLOCK + lane] = v;
+    } else if (t.sp - S < a.spill_depth) {
+        a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid] = v;
+    } else {
+        overflow = true;
+        return;
+    }
+    ++t.sp;
+}
+
+template <int BLOCK, int S>
+__device__ __forceinline__ int popw(const TraceArgs& a, Trav3& t, const int* __restrict__ stk, int lane, uint32_t gid) {
+    --t.sp;
+    if (t.sp < S) return stk[t.sp * BLOCK + lane];
+    return a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid];
+}
+
 // Coded node step (nodes from TraceArgs::cnodes, code_nodes in arx_bvh.hpp): a child word is
 // already a stack entry (inner >= 0, leaf < 0, empty = -1 = a 0-triangle leaf), so the step
 // is "hit or not" per child and one nearest-first choice: the nearer hit child is next (a
 // leaf becomes the pending leaf), the farther one is pushed.  (A v_med3 clamp of the z slab
 // looks cheaper but accepts every box behind the ray / beyond the hit that is entered through
 // a z face with tn == tf: 4x the leaf tests.)  Requires t.pc == 0.
-template <int BLOCK, int STACK>
+// BUF: fetch through a buffer resource (32-bit offsets, no 64-bit address VALU), and only the
+// 56 bytes the step uses (the compiler widens a plain 8-byte tail load to 16 bytes).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const BvhNode* nodes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<BvhNode*>(nodes), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// SPILL: STACK LDS entries + the global spill column (pushw / popw).
+template <int BLOCK, int STACK, bool BUF = false, bool SPILL = false>
 __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
-                                           int* __restrict__ stk, int lane, bool& overflow) {
+                                           int* __restrict__ stk, int lane, bool& overflow,
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t gid = 0) {
     if (t.node < 0) {  // pop
-        --t.sp;
-        const int e = stk[t.sp * BLOCK + lane];
+        int e;
+        if constexpr (SPILL) {
+            e = popw<BLOCK, STACK>(a, t, stk, lane, gid);
+        } else {
+            --t.sp;
+            e = stk[t.sp * BLOCK + lane];
+        }
         if (e < 0) {
             const int v = ~e;
             t.pf = v >> 4;
@@ -741,11 +777,21 @@ __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, flo
         }
         t.node = e;
     }
-    const float4* np = reinterpret_cast<const float4*>(a.cnodes + t.node);
-    const float4 na = np[0];
-    const float4 nb = np[1];
-    const float4 nc = np[2];
-    const int2 nd = *reinterpret_cast<const int2*>(np + 3);
+    float4 na, nb, nc;
+    int2 nd;
+    if constexpr (BUF) {
+        const int off = t.node * (int)sizeof(BvhNode);
+        na = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        nb = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        nc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 0));
+        nd = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(rs, off + 48, 0, 0));
+    } else {
+        const float4* np = reinterpret_cast<const float4*>(a.cnodes + t.node);
+        na = np[0];
+        nb = np[1];
+        nc = np[2];
+        nd = *reinterpret_cast<const int2*>(np + 3);
+    }
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
     const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
     const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
@@ -760,11 +806,113 @@ __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, flo
     const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
     const bool near1 = h1 && (!h0 || tn1 < tn0);
     const int next = (h0 || h1) ? (near1 ? nd.y : nd.x) : -1;
-    if (h0 && h1) push3<BLOCK, STACK>(t, stk, lane, near1 ? nd.x : nd.y, overflow);
+    if (h0 && h1) {
+        if constexpr (SPILL)
+            pushw<BLOCK, STACK>(a, t, stk, lane, gid, near1 ? nd.x : nd.y, overflow);
+        else
+            push3<BLOCK, STACK>(t, stk, lane, near1 ? nd.x : nd.y, overflow);
+    }
     // next >= 0: visit it; next < 0: a leaf (or -1: nothing) becomes the pending leaf, pop after
     const int v = ~next;
     t.node = next < 0 ? -1 : next;
     t.pf = v >> 4;                 // don't care while pc == 0
+    t.pc = next < 0 ? (v & 15) : 0;
+}
+
+// Quad-cooperative node fetch through LDS (gfx950 buffer_load_dwordx4 ... lds).  Load k makes
+// lane 4q+i fetch 16-B chunk i of quad-member k's node, so each wave-instruction touches 16
+// distinct 64-B lines instead of 64 (the vector-memory address path is charged per line);
+// the data lands in the wave's LDS stage as [k][lane] 16-B slots, i.e. the node of lane 4q+k
+// is the 64 contiguous bytes at k*1024 + q*64.  Wave-wide: every lane passes a node (lanes
+// without one pass 0 and ignore the result).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void coop_fetch_lds(__amdgpu_buffer_rsrc_t rs, int node, int wl, int* stage) {
+    const int c = (wl & 3) * 16;
+    const int s0 = __builtin_amdgcn_mov_dpp(node, 0x00, 0xF, 0xF, false);
+    const int s1 = __builtin_amdgcn_mov_dpp(node, 0x55, 0xF, 0xF, false);
+    const int s2 = __builtin_amdgcn_mov_dpp(node, 0xAA, 0xF, 0xF, false);
+    const int s3 = __builtin_amdgcn_mov_dpp(node, 0xFF, 0xF, 0xF, false);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(stage), 16, s0 * 64 + c, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(stage + 256), 16, s1 * 64 + c, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(stage + 512), 16, s2 * 64 + c, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(stage + 768), 16, s3 * 64 + c, 0, 0, 0);
+}
+
+// node_step7 (coded nodes, spill stack) with the cooperative fetch.  Called by all lanes of
+// the wave; `go` marks the lanes that take a step (t.pc == 0 and work left).
+// CHECK 1: count lanes present at the fetch + compare with a direct load; 2: compare only.
+// FIX (read-after-DMA experiments): 1 explicit vmcnt(0) + s_nop delay, 2 explicit vmcnt(0),
+// 3 dword LDS reads.
+template <int BLOCK, int STACK, int CHECK = 0, int FIX = 0>
+__device__ __forceinline__ void node_step9(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, bool& overflow,
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t gid, int* stage, bool go) {
+    if constexpr (CHECK == 1) {  // lanes present at the wave-wide fetch
+        const int present = __popcll(__ballot(true));
+        if ((lane & 63) == 0) atomicAdd(a.counters + 12, (unsigned long long)present);
+        if ((lane & 63) == 0) atomicAdd(a.counters + 13, 1ull);
+    }
+    bool fetch = go;
+    if (go && t.node < 0) {  // pop
+        const int e = popw<BLOCK, STACK>(a, t, stk, lane, gid);
+        if (e < 0) {
+            const int v = ~e;
+            t.pf = v >> 4;
+            t.pc = v & 15;
+            fetch = false;
+        } else {
+            t.node = e;
+        }
+    }
+    const int wl = lane & 63;
+    coop_fetch_lds(rs, fetch ? t.node : 0, wl, stage);
+    if constexpr (FIX == 1) asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (FIX == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!fetch) return;
+    float4 na, nb, nc;
+    int2 nd;
+    if constexpr (FIX == 3) {
+        const volatile int* sv = stage + (wl & 3) * 256 + (wl >> 2) * 16;
+        na = make_float4(__int_as_float(sv[0]), __int_as_float(sv[1]), __int_as_float(sv[2]), __int_as_float(sv[3]));
+        nb = make_float4(__int_as_float(sv[4]), __int_as_float(sv[5]), __int_as_float(sv[6]), __int_as_float(sv[7]));
+        nc = make_float4(__int_as_float(sv[8]), __int_as_float(sv[9]), __int_as_float(sv[10]), __int_as_float(sv[11]));
+        nd = make_int2(sv[12], sv[13]);
+    } else {
+        const int4* sp = reinterpret_cast<const int4*>(stage + (wl & 3) * 256 + (wl >> 2) * 16);
+        na = __builtin_bit_cast(float4, sp[0]);
+        nb = __builtin_bit_cast(float4, sp[1]);
+        nc = __builtin_bit_cast(float4, sp[2]);
+        nd = *reinterpret_cast<const int2*>(sp + 3);
+    }
+    if constexpr (CHECK > 0) {
+        const float4* np = reinterpret_cast<const float4*>(a.cnodes + t.node);
+        const float4 ra = np[0], rb = np[1], rc = np[2];
+        const int2 rd = *reinterpret_cast<const int2*>(np + 3);
+        const bool same = ra.x == na.x && ra.y == na.y && ra.z == na.z && ra.w == na.w && rb.x == nb.x &&
+                          rb.y == nb.y && rb.z == nb.z && rb.w == nb.w && rc.x == nc.x && rc.y == nc.y &&
+                          rc.z == nc.z && rc.w == nc.w && rd.x == nd.x && rd.y == nd.y;
+        if (!same) atomicAdd(a.counters + 14, 1ull);
+        atomicAdd(a.counters + 15, 1ull);
+    }
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+    const bool near1 = h1 && (!h0 || tn1 < tn0);
+    const int next = (h0 || h1) ? (near1 ? nd.y : nd.x) : -1;
+    if (h0 && h1) pushw<BLOCK, STACK>(a, t, stk, lane, gid, near1 ? nd.x : nd.y, overflow);
+    const int v = ~next;
+    t.node = next < 0 ? -1 : next;
+    t.pf = v >> 4;
     t.pc = next < 0 ? (v & 15) : 0;
 }
 
@@ -1023,6 +1171,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
     if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
+    constexpr bool COOP = NS >= 80;  // cooperative LDS fetch (node_step9)
+    constexpr int kCheck9 = (NS >= 100 && NS < 120) ? 1 : (NS >= 120 && NS < 140) ? 2 : 0;
+    constexpr int kFix9 = NS >= 180 ? 3 : NS >= 160 ? 2 : NS >= 140 ? 1 : 0;
+    __shared__ __attribute__((aligned(16))) int stage_all[COOP ? BLOCK * 16 : 4];
+    int* const stage = stage_all + (COOP ? (threadIdx.x >> 6) * 1024 : 0);
+    const __amdgpu_buffer_rsrc_t nrs = node_rsrc(a.cnodes);  // coded nodes (NS >= 40)
+    const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;     // spill column (NS >= 60)
     // MIG > 0: block-level ray migration (see migrate comment below); LDS queue of parked rays
     constexpr int MQ = MIG > 0 ? 64 : 1;
     __shared__ float4 mq_a[MQ], mq_b[MQ];
@@ -1038,11 +1193,29 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     }
     const int lane = threadIdx.x;
     const uint64_t n = a.pool_from < 0 ? a.ray_end - a.ray_begin : a.stash_count[a.pool_from];
-    // static per-wave ranges (a.static_ranges): wave w owns pool entries [w_next, w_end)
+    // static per-wave ranges (a.static_ranges): wave w owns pool entries [w_next, w_end).
+    // 1: n / n_waves each; 2: whole 64-ray chunks spread evenly (a wave's last round is full,
+    // not a few lanes); 3: whole chunks, the surplus chunks on the first waves.
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint64_t w_next = n * wave_id / n_waves;
-    const uint64_t w_end = n * (wave_id + 1) / n_waves;
+    uint64_t w_next, w_end;
+    if (a.static_ranges >= 2) {
+        const uint64_t chunks = (n + 63) / 64;
+        uint64_t c0, c1;
+        if (a.static_ranges == 2) {
+            c0 = chunks * wave_id / n_waves;
+            c1 = chunks * (wave_id + 1) / n_waves;
+        } else {
+            const uint64_t q = chunks / n_waves, rem = chunks % n_waves;
+            c0 = q * wave_id + min((uint64_t)wave_id, rem);
+            c1 = c0 + q + (wave_id < rem ? 1 : 0);
+        }
+        w_next = min(n, 64 * c0);
+        w_end = min(n, 64 * c1);
+    } else {
+        w_next = n * wave_id / n_waves;
+        w_end = n * (wave_id + 1) / n_waves;
+    }
     bool draining = false;
     unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
@@ -1218,11 +1391,25 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     d_pend += __popcll(m_leaf);
                     d_inact += __popcll(__ballot(!active));
                 }
-                if constexpr (NS == 6) {
+                if constexpr (COOP) {  // wave-wide steps: 1 + NS % 20
+                    node_step9<BLOCK, STACK, kCheck9, kFix9>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid, stage,
+                                                          can_node);
+#pragma unroll
+                    for (int k = 0; k < NS % 20; ++k) {
+                        const bool go = can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0);
+                        if (__ballot(go) == 0ull) break;
+                        node_step9<BLOCK, STACK, kCheck9, kFix9>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid,
+                                                              stage, go);
+                    }
+                } else if constexpr (NS == 6) {
                     node_step6<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, can_node);  // all lanes
                 } else if (can_node) {
-                    if constexpr (NS >= 20)
-                        node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                    if constexpr (NS >= 60)
+                        node_step7<BLOCK, STACK, true, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid);
+                    else if constexpr (NS >= 40)
+                        node_step7<BLOCK, STACK, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs);
+                    else if constexpr (NS >= 20)
+                        node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs);
                     else if constexpr (NS == 5)
                         node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else if constexpr (NS == 7)
@@ -1230,11 +1417,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     else
                         node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                 }
-                if constexpr (NS >= 20) {  // coded node step + NS - 20 extra steps
+                if constexpr (COOP) {
+                } else if constexpr (NS >= 20) {  // coded node step + NS % 20 extra steps (NS >= 40: buffer loads)
 #pragma unroll
-                    for (int k = 0; k < NS - 20; ++k) {
+                    for (int k = 0; k < NS % 20; ++k) {
                         if (can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0))
-                            node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
+                            node_step7<BLOCK, STACK, (NS >= 40), (NS >= 60)>(a, r, oix, oiy, oiz, t, stk, lane, overflow,
+                                                                             nrs, gid);
                     }
                 } else if constexpr (NS >= 8) {
                     // Extra node steps for lanes that can go on, without the loop control above:
@@ -1303,27 +1492,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
 // visited next, the nearest leaf is parked as the pending leaf, and the rest are pushed far
 // to near.  The stack keeps S entries per lane in LDS and spills deeper entries to a
 // per-lane global region sized on the host for the tree's worst case.
-template <int BLOCK, int S>
-__device__ __forceinline__ void pushw(const TraceArgs& a, Trav3& t, int* __restrict__ stk, int lane, uint32_t gid, int v,
-                                      bool& overflow) {
-    if (t.sp < S) {
-        stk[t.sp * BLOCK + lane] = v;
-    } else if (t.sp - S < a.spill_depth) {
-        a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid] = v;
-    } else {
-        overflow = true;
-        return;
-    }
-    ++t.sp;
-}
-
-template <int BLOCK, int S>
-__device__ __forceinline__ int popw(const TraceArgs& a, Trav3& t, const int* __restrict__ stk, int lane, uint32_t gid) {
-    --t.sp;
-    if (t.sp < S) return stk[t.sp * BLOCK + lane];
-    return a.spill[(uint64_t)(t.sp - S) * a.spill_lanes + gid];
-}
-
 __device__ __forceinline__ void cswap(float& ka, int& va, float& kb, int& vb) {
     const bool sw = kb < ka;
     const float k = sw ? kb : ka;
@@ -1695,9 +1863,10 @@ template <int BLOCK, int THRESH, int LEAF_THRESH, int STACK = kStackDepth, int M
           int NS = 3, int REFILL = 0, int MIG = 0>
 hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
     TraceArgs a = args;
-    // REFILL bit 0: directions from a pre-pass; bit 1: static per-wave ranges
+    // REFILL bit 0: directions from a pre-pass; bit 1: static per-wave ranges, bit 2 / 3 in
+    // whole 64-ray chunks, spread / surplus first (see trace_kernel_v3)
     a.dirs = nullptr;
-    a.static_ranges = (REFILL & 2) ? 1 : 0;
+    a.static_ranges = (REFILL & 2) ? ((REFILL & 4) ? 2 : (REFILL & 8) ? 3 : 1) : 0;
     const uint64_t n_rays = a.ray_end - a.ray_begin;
     if ((REFILL & 1) && a.dirs_buf && n_rays <= a.dirs_cap && n_rays > 0) {
         const uint64_t g = (n_rays + 255) / 256;
@@ -1706,7 +1875,16 @@ hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
         a.dirs = a.dirs_buf;
     }
     auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS, MIG>;
-    const int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
+    int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
+    if constexpr (NS >= 60) {  // STACK LDS entries, the rest of the worst case (bvh_depth) spills (NS >= 80 too)
+        a.spill_depth = a.bvh_depth + 1 > STACK ? a.bvh_depth + 1 - STACK : 0;
+        if (a.spill_depth > 0) {
+            if (!a.spill) return hipErrorInvalidValue;
+            const uint64_t max_grid = a.spill_lanes / BLOCK;  // every lane owns a spill column
+            if ((uint64_t)grid > max_grid) grid = (int)max_grid;
+            if (grid <= 0) return hipErrorInvalidValue;
+        }
+    }
     const int phases = (a.stash[0] && a.stash[1] && a.stash_count) ? std::max(1, env_int("ARX_PHASES", 1)) : 1;
     const int low = env_int("ARX_DRAIN_LOW", 32);
     if ((uint64_t)grid * BLOCK > a.stash_cap && phases > 1) return hipErrorInvalidValue;
@@ -1927,6 +2105,44 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 767: return launch_v3<128, 12, 12, 28, 5, false, 1, 27, 3>(a, cus, s);
         case 768: return launch_v3<128, 12, 16, 28, 5, false, 1, 27, 3>(a, cus, s);
         case 769: return launch_v3<128, 12, 12, 28, 5, true, 1, 27, 3>(a, cus, s);  // instrumented
+        // coded nodes fetched through a buffer resource (56 B per node)
+        case 770: return launch_v3<128, 12, 12, 28, 5, false, 1, 47, 3>(a, cus, s);
+        case 771: return launch_v3<128, 12, 12, 28, 5, false, 1, 43, 3>(a, cus, s);
+        case 772: return launch_v3<128, 12, 12, 28, 5, false, 1, 51, 3>(a, cus, s);
+        case 773: return launch_v3<128, 12, 12, 28, 5, false, 1, 55, 3>(a, cus, s);
+        case 774: return launch_v3<128, 12, 16, 28, 5, false, 1, 47, 3>(a, cus, s);
+        case 775: return launch_v3<128, 16, 12, 28, 5, false, 1, 47, 3>(a, cus, s);
+        case 776: return launch_v3<128, 12, 12, 28, 5, false, 1, 31, 3>(a, cus, s);
+        case 779: return launch_v3<128, 12, 12, 28, 5, true, 1, 47, 3>(a, cus, s);  // instrumented
+        // whole-chunk static ranges
+        case 780: return launch_v3<128, 12, 12, 28, 5, false, 1, 51, 7>(a, cus, s);
+        case 781: return launch_v3<128, 12, 12, 28, 5, false, 1, 51, 11>(a, cus, s);
+        case 782: return launch_v3<128, 12, 12, 28, 5, false, 1, 47, 7>(a, cus, s);
+        case 783: return launch_v3<128, 16, 12, 28, 5, false, 1, 51, 7>(a, cus, s);
+        case 784: return launch_v3<128, 8, 12, 28, 5, false, 1, 51, 7>(a, cus, s);
+        case 789: return launch_v3<128, 12, 12, 28, 5, true, 1, 51, 7>(a, cus, s);  // instrumented
+        // short LDS stack + global spill column (NS >= 60) at higher occupancy targets
+        case 792: return launch_v3<128, 12, 12, 16, 5, false, 1, 71, 3>(a, cus, s);
+        case 793: return launch_v3<128, 12, 12, 16, 6, false, 1, 71, 3>(a, cus, s);
+        case 794: return launch_v3<128, 12, 12, 16, 8, false, 1, 71, 3>(a, cus, s);
+        case 795: return launch_v3<128, 12, 12, 20, 6, false, 1, 71, 3>(a, cus, s);
+        case 796: return launch_v3<128, 12, 12, 12, 8, false, 1, 71, 3>(a, cus, s);
+        case 797: return launch_v3<128, 12, 12, 16, 7, false, 1, 71, 3>(a, cus, s);
+        // cooperative LDS node fetch (NS >= 80) + spill stack
+        case 850: return launch_v3<128, 12, 12, 12, 5, false, 1, 91, 3>(a, cus, s);
+        case 851: return launch_v3<128, 12, 12, 16, 5, false, 1, 91, 3>(a, cus, s);
+        case 852: return launch_v3<128, 12, 12, 12, 5, false, 1, 87, 3>(a, cus, s);
+        case 853: return launch_v3<128, 12, 12, 12, 5, false, 1, 83, 3>(a, cus, s);
+        case 854: return launch_v3<128, 12, 12, 8, 5, false, 1, 91, 3>(a, cus, s);
+        case 855: return launch_v3<128, 12, 12, 12, 6, false, 1, 91, 3>(a, cus, s);
+        case 856: return launch_v3<128, 12, 12, 12, 4, false, 1, 91, 3>(a, cus, s);
+        case 858: return launch_v3<128, 12, 12, 12, 5, false, 1, 111, 3>(a, cus, s);  // fetch self-check
+        case 857: return launch_v3<128, 12, 12, 12, 5, false, 1, 131, 3>(a, cus, s);  // compare-only self-check
+        case 860: return launch_v3<128, 12, 12, 12, 5, false, 1, 151, 3>(a, cus, s);  // FIX 1
+        case 861: return launch_v3<128, 12, 12, 12, 5, false, 1, 171, 3>(a, cus, s);  // FIX 2
+        case 862: return launch_v3<128, 12, 12, 12, 5, false, 1, 191, 3>(a, cus, s);  // FIX 3
+        case 859: return launch_v3<128, 12, 12, 12, 5, true, 1, 91, 3>(a, cus, s);  // instrumented
+        case 863: return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(a, cus, s);  // default for deep trees
         case 749: return launch_v3<128, 12, 12, 28, 5, true, 1, 8, 3>(a, cus, s);  // instrumented
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
@@ -1952,10 +2168,12 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 327: return launch_w<kWideQ4, 128, 24, 32, 24, 5>(a, cus, s);
         case 328: return launch_w<kWideQ4, 256, 24, 64, 12, 5>(a, cus, s);
         case 329: return launch_w<kWideQ4, 128, 28, 32, 12, 5>(a, cus, s);
-        default:  // = 706: static per-wave ray ranges, direction pre-pass, refill at 12 idle lanes
-            if (a.bvh_depth < 28) return launch_v3<128, 12, 12, 28, 5, false, 1, 3, 3>(a, cus, s);
-            if (a.bvh_depth < 40) return launch_v3<128, 12, 12, 40, 5, false, 1, 3, 3>(a, cus, s);
-            return launch_v3<128, 12, 12, kMaxStackDepth, 5, false, 1, 3, 3>(a, cus, s);
+        default:  // = 772: static per-wave ray ranges, direction pre-pass, refill at 12 idle lanes,
+                  // coded nodes through a buffer resource, 12 node steps per inner iteration;
+                  // trees deeper than the 28-entry LDS stack spill to a global column (same
+                  // occupancy) instead of taking a bigger LDS stack
+            if (a.bvh_depth < 28) return launch_v3<128, 12, 12, 28, 5, false, 1, 51, 3>(a, cus, s);
+            return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(a, cus, s);
     }
 }
 
