@@ -29,6 +29,19 @@ struct BuildParams {
     int leaf_max = 4;        // SAH may stop at <= leaf_max triangles (always splits above)
     float trav_cost = 1.0f;  // SAH cost of a node step relative to ...
     float isect_cost = 1.0f; // ... one triangle test
+    // Spatial splits (SBVH, Stich, Friedrich & Dietrich 2009): a triangle may be referenced by
+    // several leaves, each bounding only its clipped part.  Tried at nodes whose best object
+    // split leaves children overlapping by more than spatial_alpha of the root's area, while
+    // the references stay below (1 + spatial_budget) x the triangle count.
+    bool spatial = true;
+    float spatial_alpha = 1e-3f;
+    float spatial_budget = 3.0f;
+    int spatial_max_depth = 64;  // spatial splits only above this depth
+    // Depth cap of the spatial builder: once depth + log2(refs / leaf_max) reaches it, nodes are
+    // split at the object median of their widest centroid axis, so every leaf sits at depth <=
+    // max_depth (the kernel's 28-entry LDS stack then needs no spill path).
+    int max_depth = 26;
+    int threads = 8;  // top-level subtrees built concurrently (spatial builder)
 };
 BuildParams& build_params();
 
@@ -48,9 +61,24 @@ bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size
                         const char** why);
 // Coded copy of validated nodes for the coded node step: d = (code0, code1, 0, 0) with
 // code = inner node index (>= 0), ~(first*16 + count) for a leaf (< 0; the traversal-stack
-// entry format), or -1 for an empty child (a leaf of 0 triangles, i.e. a no-op if its
-// inverted box ever passes the slab test).  Boxes are unchanged.
+// entry format), or kEmptyChildCode for an empty child: a leaf of 0 triangles, i.e. a no-op if
+// its inverted box ever passes the slab test (-1 is kept free: it means "no entry").  Boxes are
+// unchanged.
+constexpr int32_t kEmptyChildCode = ~16;
 void code_nodes(const BvhNode* in, size_t n, BvhNode* out);
+// Grid for QNode2 trees covering the box [lo, hi] (scene, receiver and emitter) with a margin
+// of 1/10 of the largest extent on every side, so listener moves inside the room keep the grid.
+QGrid make_qgrid(const float lo[3], const float hi[3]);
+// True if the box [lo, hi] lies inside the grid with room for the outward rounding.
+bool qgrid_contains(const QGrid& g, const float lo[3], const float hi[3]);
+// Quantized copy of coded nodes: every child box is rounded outward to the grid with a margin of
+// 0.1 step (for the kernel's f32 slab arithmetic, see arx_trace.hip node_step7);
+// empty children become a one-step box at the grid corner.  False if a box leaves the grid.
+bool quantize_nodes16(const BvhNode* coded, size_t n, const QGrid& g, QNode2* out);
+// Octant copy of quantized nodes for rays whose direction has sign bits `octant` (bit k set:
+// negative component k): every axis word is (near | far << 16), i.e. lo and hi swapped on the
+// negative axes, so the slab test needs no min/max.  Octant 0 is the plain layout.
+void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out);
 
 // Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
 struct WideBuild {

@@ -80,6 +80,9 @@ struct arx_renderer {
     // device
     BvhNode* d_nodes = nullptr;
     BvhNode* d_cnodes = nullptr;  // coded copy (code_nodes), same indices
+    QNode2* d_qnodes = nullptr;   // 16-bit quantized copies of d_cnodes: 8 octants x nodes_cap
+    QGrid qgrid{};
+    bool qgrid_set = false;
     size_t nodes_cap = 0;
     TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
@@ -248,11 +251,14 @@ arx_status ensure_device_scene(arx_renderer* r) {
     if (n_nodes > r->nodes_cap) {
         if (r->d_nodes) ARX_HIP(hipFree(r->d_nodes));
         if (r->d_cnodes) ARX_HIP(hipFree(r->d_cnodes));
+        if (r->d_qnodes) ARX_HIP(hipFree(r->d_qnodes));
         r->d_nodes = nullptr;
         r->d_cnodes = nullptr;
+        r->d_qnodes = nullptr;
         size_t cap = n_nodes + 1024;
         ARX_HIP(hipMalloc(&r->d_nodes, cap * sizeof(BvhNode)));
         ARX_HIP(hipMalloc(&r->d_cnodes, cap * sizeof(BvhNode)));
+        ARX_HIP(hipMalloc(&r->d_qnodes, 8 * cap * sizeof(QNode2)));
         r->nodes_cap = cap;
         full = true;
     }
@@ -264,7 +270,26 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
-    if (full || r->recv_dirty) {
+    // quantized copy: a new grid (and a full re-quantization) when the scene changed or the
+    // receiver left the grid; the emitter is checked per launch (arx_trace_rays)
+    bool requant = full || !r->qgrid_set;
+    if (!requant && r->recv_dirty && r->recv.root.count >= 0 &&
+        !qgrid_contains(r->qgrid, r->recv.root.lo, r->recv.root.hi))
+        requant = true;
+    if (requant) {
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = hi[k] = r->emitter[k];
+            for (const ChildRef* c : {&r->scene.root, &r->recv.root}) {
+                if (c->count < 0) continue;  // empty part
+                lo[k] = std::min(lo[k], c->lo[k]);
+                hi[k] = std::max(hi[k], c->hi[k]);
+            }
+        }
+        r->qgrid = make_qgrid(lo, hi);
+        r->qgrid_set = true;
+    }
+    if (full || r->recv_dirty || requant) {
         BvhNode top = make_node(r->scene.root, r->recv.root);
         {
             // structure check (acyclic, in range): the scene part when it changed, the receiver
@@ -284,13 +309,37 @@ arx_status ensure_device_scene(arx_renderer* r) {
         code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
         ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-        if (full && !r->scene.nodes.empty()) {
+        QNode2 qtop;
+        std::vector<QNode2> qscene, qrecv(crecv.size());
+        if (!quantize_nodes16(&ctop, 1, r->qgrid, &qtop) ||
+            !quantize_nodes16(crecv.data(), crecv.size(), r->qgrid, qrecv.data()))
+            return fail(ARX_ERR_INTERNAL, "BVH quantization failed (box outside the grid)");
+        // the 8 octant copies of quantized nodes [at, at + n); host images live until the sync
+        std::vector<std::vector<QNode2>> qoct;
+        auto upload_q = [&](const QNode2* q, size_t n, size_t at) -> hipError_t {
+            hipError_t e = hipMemcpyAsync(r->d_qnodes + at, q, n * sizeof(QNode2), hipMemcpyHostToDevice, r->stream);
+            for (int o = 1; o < 8 && e == hipSuccess; ++o) {
+                qoct.emplace_back(n);
+                octant_nodes16(q, n, o, qoct.back().data());
+                e = hipMemcpyAsync(r->d_qnodes + (size_t)o * r->nodes_cap + at, qoct.back().data(), n * sizeof(QNode2),
+                                   hipMemcpyHostToDevice, r->stream);
+            }
+            return e;
+        };
+        ARX_HIP(upload_q(&qtop, 1, 0));
+        if ((full || requant) && !r->scene.nodes.empty()) {
             cscene.resize(r->scene.nodes.size());
             code_nodes(r->scene.nodes.data(), r->scene.nodes.size(), cscene.data());
-            ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(), r->scene.nodes.size() * sizeof(BvhNode),
-                                   hipMemcpyHostToDevice, r->stream));
-            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
-                                   hipMemcpyHostToDevice, r->stream));
+            if (full) {
+                ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(),
+                                       r->scene.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+                ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
+                                       hipMemcpyHostToDevice, r->stream));
+            }
+            qscene.resize(cscene.size());
+            if (!quantize_nodes16(cscene.data(), cscene.size(), r->qgrid, qscene.data()))
+                return fail(ARX_ERR_INTERNAL, "BVH quantization failed (scene box outside the grid)");
+            ARX_HIP(upload_q(qscene.data(), qscene.size(), 1));
         }
         if (full && !r->scene.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
@@ -300,6 +349,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
                                    r->recv.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
             ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
                                    crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+            ARX_HIP(upload_q(qrecv.data(), qrecv.size(), 1 + r->scene.nodes.size()));
         }
         if (!r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
@@ -430,6 +480,7 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_live_out);
     hipFree(r->d_nodes);
     hipFree(r->d_cnodes);
+    hipFree(r->d_qnodes);
     hipFree(r->d_tris);
     hipFree(r->d_wnodes);
     hipFree(r->d_spill);
@@ -560,6 +611,14 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     std::memset(&a, 0, sizeof(a));
     a.nodes = r->d_nodes;
     a.cnodes = r->d_cnodes;
+    {
+        // quantized nodes only while the emitter (the one ray origin off the geometry) is on the
+        // grid: the slab arithmetic's error bound assumes origins within the grid's extent
+        const float* e = r->emitter;
+        a.qnodes = (r->qgrid_set && qgrid_contains(r->qgrid, e, e)) ? r->d_qnodes : nullptr;
+        a.qgrid = r->qgrid;
+        a.qostride = (uint32_t)r->nodes_cap;
+    }
     a.tris = r->d_tris;
     a.hist = r->hist();
     a.counters = r->d_counters;

@@ -68,6 +68,23 @@ static_assert(sizeof(QNode4) == 64, "QNode4 must be 64 B");
 // Node-format code of QNode4 trees where a "width" is passed (2, 4, 8 are BvhNode / WideNode<W>).
 constexpr int kWideQ4 = 5;
 
+// 16-bit quantized binary node, 32 B (2 x 16-B loads instead of 3.5 for the f32 node): the
+// coded node (code_nodes) with both child boxes on one scene-wide 16-bit grid per axis,
+// plane = grid.origin + q * grid.scale (real arithmetic), rounded outward with a 0.1-step margin so
+// the kernel's f32 slab arithmetic stays conservative (quantize_nodes16, arx_bvh.cpp).
+//   q[0..2] = child 0 x, y, z as (lo | hi << 16); q[3..5] = child 1; code[2] as in code_nodes.
+struct alignas(16) QNode2 {
+    uint32_t q[6];
+    int32_t code[2];
+};
+static_assert(sizeof(QNode2) == 32, "QNode2 must be 32 B");
+
+// The scene-wide grid of QNode2 trees.
+struct QGrid {
+    float origin[3];
+    float scale[3];
+};
+
 // LDS traversal stack depth per lane; the builder caps tree depth below it.
 constexpr int kStackDepth = 40;      // v1/v2 (A/B variants): trees up to depth 39
 constexpr int kMaxStackDepth = 64;   // deepest stack variant of the default kernel
@@ -119,6 +136,12 @@ struct TraceArgs {
     uint64_t dirs_cap;
     // coded copy of `nodes` (code_nodes, arx_bvh.hpp): d = (code0, code1, 0, 0)
     const BvhNode* cnodes;
+    // 16-bit quantized copy of cnodes (QNode2, same indices) and its grid; kernel variants
+    // with quantized nodes fall back to cnodes when qnodes is null (see launch_v3)
+    const QNode2* qnodes;
+    QGrid qgrid;
+    // octant copies (octant_nodes16): copy o of node i at qnodes[o * qostride + i], o = 0 plain
+    uint32_t qostride;
 };
 
 }  // namespace arx

@@ -745,7 +745,7 @@ __device__ __forceinline__ int popw(const TraceArgs& a, Trav3& t, const int* __r
 }
 
 // Coded node step (nodes from TraceArgs::cnodes, code_nodes in arx_bvh.hpp): a child word is
-// already a stack entry (inner >= 0, leaf < 0, empty = -1 = a 0-triangle leaf), so the step
+// already a stack entry (inner >= 0, leaf < 0, empty = kEmptyChildCode = a 0-triangle leaf), so the step
 // is "hit or not" per child and one nearest-first choice: the nearer hit child is next (a
 // leaf becomes the pending leaf), the farther one is pushed.  (A v_med3 clamp of the z slab
 // looks cheaper but accepts every box behind the ray / beyond the hit that is entered through
@@ -757,7 +757,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const BvhNode* nodes
 }
 
 // SPILL: STACK LDS entries + the global spill column (pushw / popw).
-template <int BLOCK, int STACK, bool BUF = false, bool SPILL = false>
+// Q16: 32-B QNode2 nodes (two 16-B loads; rs over TraceArgs::qnodes).  A slab plane is
+// grid.origin + q * grid.scale, so t = (origin + q*scale - o) * inv = q * (scale*inv) +
+// (origin - o)*inv: the caller passes ix = scale*inv and oix = (o - origin)*inv per axis, and the
+// step is the same fma per plane after one u16 -> f32 conversion.  Conservative: the f32 error
+// of that form is below 5 * 2^-24 * (grid extent) * |inv| for origins on the grid, far below the
+// 0.1-step outward margin of every quantized plane (quantize_nodes16; the emitter is checked per launch).
+template <int BLOCK, int STACK, bool BUF = false, bool SPILL = false, bool Q16 = false>
 __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, float oix, float oiy, float oiz, Trav3& t,
                                            int* __restrict__ stk, int lane, bool& overflow,
                                            __amdgpu_buffer_rsrc_t rs, uint32_t gid = 0) {
@@ -779,7 +785,17 @@ __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, flo
     }
     float4 na, nb, nc;
     int2 nd;
-    if constexpr (BUF) {
+    if constexpr (Q16) {
+        const int off = t.node * (int)sizeof(QNode2);
+        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        // same register roles as the f32 node: na = (x0 lo, x0 hi, y0 lo, y0 hi), nb = child 1,
+        // nc = (z0 lo, z0 hi, z1 lo, z1 hi)
+        na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
+        nb = make_float4((float)(A.w & 0xffffu), (float)(A.w >> 16), (float)(B.x & 0xffffu), (float)(B.x >> 16));
+        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
+        nd = make_int2((int)B.z, (int)B.w);
+    } else if constexpr (BUF) {
         const int off = t.node * (int)sizeof(BvhNode);
         na = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         nb = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
@@ -1171,12 +1187,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
     uint64_t c_outer = 0, c_node = 0, c_leaf = 0, c_mark = 0;  // DBG: s_memtime cycles per phase
     if constexpr (DBG) c_mark = __builtin_amdgcn_s_memtime();
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: dummy target of branch-free pushes
-    constexpr bool COOP = NS >= 80;  // cooperative LDS fetch (node_step9)
-    constexpr int kCheck9 = (NS >= 100 && NS < 120) ? 1 : (NS >= 120 && NS < 140) ? 2 : 0;
-    constexpr int kFix9 = NS >= 180 ? 3 : NS >= 160 ? 2 : NS >= 140 ? 1 : 0;
+    // NS >= 200: the NS - 200 step scheme over 16-bit quantized QNode2 nodes (NS - 200 >= 40)
+    constexpr bool QN = NS >= 200;
+    constexpr int NSB = QN ? NS - 200 : NS;
+    static_assert(!QN || (NSB >= 40 && NSB < 80), "quantized nodes: buffer-load coded steps only");
+    constexpr bool COOP = NSB >= 80;  // cooperative LDS fetch (node_step9)
+    constexpr int kCheck9 = (NSB >= 100 && NSB < 120) ? 1 : (NSB >= 120 && NSB < 140) ? 2 : 0;
+    constexpr int kFix9 = NSB >= 180 ? 3 : NSB >= 160 ? 2 : NSB >= 140 ? 1 : 0;
     __shared__ __attribute__((aligned(16))) int stage_all[COOP ? BLOCK * 16 : 4];
     int* const stage = stage_all + (COOP ? (threadIdx.x >> 6) * 1024 : 0);
-    const __amdgpu_buffer_rsrc_t nrs = node_rsrc(a.cnodes);  // coded nodes (NS >= 40)
+    const __amdgpu_buffer_rsrc_t nrs =  // coded nodes (NS >= 40) or their quantized copy
+        QN ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
+           : node_rsrc(a.cnodes);
     const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;     // spill column (NS >= 60)
     // MIG > 0: block-level ray migration (see migrate comment below); LDS queue of parked rays
     constexpr int MQ = MIG > 0 ? 64 : 1;
@@ -1353,9 +1375,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
         if (active && !trav) {
             ++n_q;
             setup_ray(r, s.pos, s.dir);
-            oix = r.o[0] * r.inv[0];
-            oiy = r.o[1] * r.inv[1];
-            oiz = r.o[2] * r.inv[2];
+            if constexpr (QN) {  // grid form of the slab planes (node_step7 Q16)
+                oix = (r.o[0] - a.qgrid.origin[0]) * r.inv[0];
+                oiy = (r.o[1] - a.qgrid.origin[1]) * r.inv[1];
+                oiz = (r.o[2] - a.qgrid.origin[2]) * r.inv[2];
+                r.inv[0] *= a.qgrid.scale[0];
+                r.inv[1] *= a.qgrid.scale[1];
+                r.inv[2] *= a.qgrid.scale[2];
+            } else {
+                oix = r.o[0] * r.inv[0];
+                oiy = r.o[1] * r.inv[1];
+                oiz = r.o[2] * r.inv[2];
+            }
             t.best_t = __builtin_huge_valf();
             t.best_id = 0x7fffffff;
             t.best = -1;
@@ -1391,46 +1422,46 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     d_pend += __popcll(m_leaf);
                     d_inact += __popcll(__ballot(!active));
                 }
-                if constexpr (COOP) {  // wave-wide steps: 1 + NS % 20
+                if constexpr (COOP) {  // wave-wide steps: 1 + NSB % 20
                     node_step9<BLOCK, STACK, kCheck9, kFix9>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid, stage,
                                                           can_node);
 #pragma unroll
-                    for (int k = 0; k < NS % 20; ++k) {
+                    for (int k = 0; k < NSB % 20; ++k) {
                         const bool go = can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0);
                         if (__ballot(go) == 0ull) break;
                         node_step9<BLOCK, STACK, kCheck9, kFix9>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid,
                                                               stage, go);
                     }
-                } else if constexpr (NS == 6) {
+                } else if constexpr (NSB == 6) {
                     node_step6<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, can_node);  // all lanes
                 } else if (can_node) {
-                    if constexpr (NS >= 60)
-                        node_step7<BLOCK, STACK, true, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid);
-                    else if constexpr (NS >= 40)
-                        node_step7<BLOCK, STACK, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs);
-                    else if constexpr (NS >= 20)
+                    if constexpr (NSB >= 60)
+                        node_step7<BLOCK, STACK, true, true, QN>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs, gid);
+                    else if constexpr (NSB >= 40)
+                        node_step7<BLOCK, STACK, true, false, QN>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs);
+                    else if constexpr (NSB >= 20)
                         node_step7<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow, nrs);
-                    else if constexpr (NS == 5)
+                    else if constexpr (NSB == 5)
                         node_step5<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
-                    else if constexpr (NS == 7)
+                    else if constexpr (NSB == 7)
                         node_step3<BLOCK, STACK, true>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                     else
                         node_step3<BLOCK, STACK>(a, r, oix, oiy, oiz, t, stk, lane, overflow);
                 }
                 if constexpr (COOP) {
-                } else if constexpr (NS >= 20) {  // coded node step + NS % 20 extra steps (NS >= 40: buffer loads)
+                } else if constexpr (NSB >= 20) {  // coded node step + NSB % 20 extra steps (NSB >= 40: buffer loads)
 #pragma unroll
-                    for (int k = 0; k < NS % 20; ++k) {
+                    for (int k = 0; k < NSB % 20; ++k) {
                         if (can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0))
-                            node_step7<BLOCK, STACK, (NS >= 40), (NS >= 60)>(a, r, oix, oiy, oiz, t, stk, lane, overflow,
+                            node_step7<BLOCK, STACK, (NSB >= 40), (NSB >= 60), QN>(a, r, oix, oiy, oiz, t, stk, lane, overflow,
                                                                              nrs, gid);
                     }
-                } else if constexpr (NS >= 8) {
+                } else if constexpr (NSB >= 8) {
                     // Extra node steps for lanes that can go on, without the loop control above:
                     // NS 8/9/10 = 1/2/3 extra steps; NS 11/12 = up to 3 while >= 24/16 lanes can;
                     // NS 13/14 = 5/7 extra; NS 15/16 = up to 7 while >= 24/32; NS 17 = up to 15 while >= 24.
-                    constexpr int kExtra = NS <= 10 ? NS - 7 : NS <= 12 ? 3 : NS == 13 ? 5 : NS <= 16 ? 7 : 15;
-                    constexpr int kMinLanes = (NS == 11 || NS == 15 || NS == 17) ? 24 : NS == 12 ? 16 : NS == 16 ? 32 : 0;
+                    constexpr int kExtra = NSB <= 10 ? NSB - 7 : NSB <= 12 ? 3 : NSB == 13 ? 5 : NSB <= 16 ? 7 : 15;
+                    constexpr int kMinLanes = (NSB == 11 || NSB == 15 || NSB == 17) ? 24 : NSB == 12 ? 16 : NSB == 16 ? 32 : 0;
 #pragma unroll
                     for (int k = 0; k < kExtra; ++k) {
                         const bool go = can_node && t.pc == 0 && (t.node >= 0 || t.sp > 0);
@@ -1450,7 +1481,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
                     ++d_lit;
                     d_ll += __popcll(m_leaf);
                 }
-                if constexpr (NS == 5) {
+                if constexpr (NSB == 5) {
                     const bool mine = trav && t.pc > 0;
                     leaf_hits_u<LV>(a.tris, r, t.pf, mine ? t.pc : 0, t.best_t, t.best_id, t.best);
                     t.pc = mine ? 0 : t.pc;
@@ -1482,6 +1513,206 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v3(TraceArgs a) {
             atomicAdd(a.counters + 6, (unsigned long long)(d_pend << 32 | (d_inact & 0xffffffffull)));
         }
     }
+}
+
+// ---- v5: branch-minimal coded traversal ---------------------------------------------------
+// t.node holds the lane's next stack entry: >= 0 an inner node (take a node step), <= -2 a
+// leaf ~(first*16 + count) (pending until the wave's leaf phase), -1 = the query is done.
+// Entries are popped at the END of a node step (and of a leaf test), so a lane at -1 has an
+// empty stack and the step guard is just `t.node >= 0`.  Inside the step every decision is a
+// select and the far child is written unconditionally (to the slot above the top of the
+// stack, or to the spare row STACK), so the only exec-mask work per step is that guard: the
+// branchy steps spent ~52 scalar instructions per step on exec masks, and the CU's one scalar
+// unit serves all 20 waves.
+// NF: node format.  0 coded BvhNode (56 B), 1 QNode2 (32 B), 2 QNode2 octant copy of this ray's
+// direction signs (obase = byte offset of that copy): each axis word is (near | far << 16), so
+// the slab test takes max / min of the near / far planes without the per-axis min/max.
+template <int BLOCK, int STACK, int NF>
+__device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                           int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs,
+                                           int obase = 0) {
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    float tn0, tf0, tn1, tf1;
+    int c0, c1;
+    if constexpr (NF == 2) {
+        const int off = obase + t.node * (int)sizeof(QNode2);
+        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        // child 0: A.x, A.y, A.z; child 1: A.w, B.x, B.y (x, y, z words)
+        const float nx0 = __builtin_fmaf((float)(A.x & 0xffffu), ix, -oix), fx0 = __builtin_fmaf((float)(A.x >> 16), ix, -oix);
+        const float ny0 = __builtin_fmaf((float)(A.y & 0xffffu), iy, -oiy), fy0 = __builtin_fmaf((float)(A.y >> 16), iy, -oiy);
+        const float nz0 = __builtin_fmaf((float)(A.z & 0xffffu), iz, -oiz), fz0 = __builtin_fmaf((float)(A.z >> 16), iz, -oiz);
+        const float nx1 = __builtin_fmaf((float)(A.w & 0xffffu), ix, -oix), fx1 = __builtin_fmaf((float)(A.w >> 16), ix, -oix);
+        const float ny1 = __builtin_fmaf((float)(B.x & 0xffffu), iy, -oiy), fy1 = __builtin_fmaf((float)(B.x >> 16), iy, -oiy);
+        const float nz1 = __builtin_fmaf((float)(B.y & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(B.y >> 16), iz, -oiz);
+        tn0 = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, 0.0f));
+        tf0 = fminf(fminf(fx0, fy0), fminf(fz0, t.best_t));
+        tn1 = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, 0.0f));
+        tf1 = fminf(fminf(fx1, fy1), fminf(fz1, t.best_t));
+        c0 = (int)B.z;
+        c1 = (int)B.w;
+    } else {
+    float4 na, nb, nc;
+    if constexpr (NF == 1) {  // QNode2 (node_step7 Q16)
+        const int off = t.node * (int)sizeof(QNode2);
+        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
+        nb = make_float4((float)(A.w & 0xffffu), (float)(A.w >> 16), (float)(B.x & 0xffffu), (float)(B.x >> 16));
+        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
+        c0 = (int)B.z;
+        c1 = (int)B.w;
+    } else {  // coded BvhNode, 56 B
+        const int off = t.node * (int)sizeof(BvhNode);
+        na = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        nb = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        nc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, 0));
+        const int2 d = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(rs, off + 48, 0, 0));
+        c0 = d.x;
+        c1 = d.y;
+    }
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    }
+    // bitwise ops on the bools: && / || would become exec-mask branches again
+    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+    const bool near1 = h1 & (!h0 | (tn1 < tn0));
+    const int c_near = near1 ? c1 : c0;
+    const int c_far = near1 ? c0 : c1;
+    // The stack never overflows: it holds at most one entry per tree level and the launcher
+    // requires STACK > bvh_depth.  The clamp only keeps the write inside the array.
+    const int sp = t.sp;
+    stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
+    asm volatile("" : "+v"(top));  // the pop read stays unconditional (no branch around it)
+    const bool any = h0 | h1;
+    const int popped = sp > 0 ? top : -1;
+    t.node = any ? c_near : popped;
+    t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
+}
+
+// Leaf phase of v5: test the pending leaf, then pop the next entry.
+template <int BLOCK, int LV>
+__device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Trav3& t, const int* __restrict__ stk,
+                                           int lane) {
+    const int v = ~t.node;
+    leaf_hits_vec<LV>(a.tris, r, v >> 4, v & 15, t.best_t, t.best_id, t.best);
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
+    asm volatile("" : "+v"(top));
+    t.node = sp > 0 ? top : -1;
+    t.sp = sp_pop;
+}
+
+// Persistent waves as v3 (static per-wave ray ranges, direction pre-pass, refill at THRESH
+// idle lanes, postponed leaves) over node_step8: NSTEPS guarded steps per inner iteration.
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1>
+__global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
+    constexpr bool Q16 = NF >= 1;
+    __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: target of writes past a full stack
+    const __amdgpu_buffer_rsrc_t nrs =
+        Q16 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
+            : node_rsrc(a.cnodes);
+    const int lane = threadIdx.x;
+    const uint64_t n = a.ray_end - a.ray_begin;
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    const uint32_t n_waves = gridDim.x * (BLOCK / 64);
+    uint64_t w_next = n * wave_id / n_waves;
+    const uint64_t w_end = n * (wave_id + 1) / n_waves;
+    uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+    const bool overflow = false;  // impossible by construction (node_step8)
+    bool active = false, trav = false, exhausted = w_next >= w_end;
+    RayState s;
+    s.depth = -1;
+    Ray r;
+    Trav3 t;
+    t.best_t = __builtin_huge_valf();
+    t.best_id = 0x7fffffff;
+    t.best = -1;
+    t.node = -1;
+    t.sp = 0;
+    t.pf = 0;
+    t.pc = 0;
+    t.visits = 0;
+    float oix = 0.f, oiy = 0.f, oiz = 0.f;
+    int obase = 0;  // NF 2: byte offset of the ray's octant copy
+    while (true) {
+        if (active && !trav) {
+            shade(a, s, r, t.best, n_rx, n_miss);
+            if (!wants_query(a, s)) active = false;
+        }
+        const unsigned long long need = __ballot(!active);
+        if (need != 0ull && !exhausted) {
+            const int cnt = __popcll(need);
+            const uint64_t base = w_next;
+            w_next += (uint64_t)cnt;
+            if (!active) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint64_t i = base + rank;
+                if (i < w_end) {
+                    ray_init(a, s, a.ray_begin + i);
+                    active = wants_query(a, s);
+                }
+            }
+            if (base + (uint64_t)cnt >= w_end) exhausted = true;
+        }
+        if (active && !trav) {
+            ++n_q;
+            setup_ray(r, s.pos, s.dir);
+            if constexpr (Q16) {  // grid form of the slab planes (node_step7 Q16)
+                oix = (r.o[0] - a.qgrid.origin[0]) * r.inv[0];
+                oiy = (r.o[1] - a.qgrid.origin[1]) * r.inv[1];
+                oiz = (r.o[2] - a.qgrid.origin[2]) * r.inv[2];
+                r.inv[0] *= a.qgrid.scale[0];
+                r.inv[1] *= a.qgrid.scale[1];
+                r.inv[2] *= a.qgrid.scale[2];
+                if constexpr (NF == 2) {
+                    const int oct = (r.inv[0] < 0.0f ? 1 : 0) | (r.inv[1] < 0.0f ? 2 : 0) | (r.inv[2] < 0.0f ? 4 : 0);
+                    obase = oct * (int)a.qostride * (int)sizeof(QNode2);
+                }
+            } else {
+                oix = r.o[0] * r.inv[0];
+                oiy = r.o[1] * r.inv[1];
+                oiz = r.o[2] * r.inv[2];
+            }
+            t.best_t = __builtin_huge_valf();
+            t.best_id = 0x7fffffff;
+            t.best = -1;
+            t.node = 0;
+            t.sp = 0;
+            trav = true;
+        }
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        while (true) {
+            if (trav && t.node == -1) trav = false;  // query done (its stack is empty)
+            const unsigned long long m_node = __ballot(t.node >= 0);
+            const unsigned long long m_leaf = __ballot(t.node <= -2);
+            if ((m_node | m_leaf) == 0ull) break;
+            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+#pragma unroll
+                for (int k = 0; k < NSTEPS; ++k)
+                    if (t.node >= 0) node_step8<BLOCK, STACK, NF>(r, oix, oiy, oiz, t, stk, lane, nrs, obase);
+            } else if (t.node <= -2) {
+                leaf_step8<BLOCK, LV>(a, r, t, stk, lane);
+            }
+        }
+    }
+    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
 }
 
 // ---------------------------------------------------------------- wide tree (v4) ---
@@ -1826,7 +2057,7 @@ int trace_block_size() { return kBlock; }
 namespace {
 // Kernel variants for A/B measurement (ARX_TRACE_KERNEL, read per launch); all are
 // bit-identical in results.  Default = the fastest measured on MI355X.
-constexpr int kDefaultVariant = 0;  // 0 = v3<128, 12, 12, stack by tree depth, 5 waves/SIMD, refill 3>
+constexpr int kDefaultVariant = 0;  // 0 = variant 921 (see launch_trace's default)
 
 template <typename K>
 int persistent_grid(K kernel, int block, uint64_t n_rays, int cus) {
@@ -1874,9 +2105,12 @@ hipError_t launch_v3(const TraceArgs& args, int cus, hipStream_t s) {
                            reinterpret_cast<float4*>(a.dirs_buf));
         a.dirs = a.dirs_buf;
     }
+    if constexpr (NS >= 200) {  // quantized nodes unavailable (emitter off the grid): the f32 coded nodes
+        if (!a.qnodes) return launch_v3<BLOCK, THRESH, LEAF_THRESH, STACK, MINW, DBG, LV, NS - 200, REFILL, MIG>(args, cus, s);
+    }
     auto k = trace_kernel_v3<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, DBG, LV, NS, MIG>;
     int grid = persistent_grid(k, BLOCK, a.ray_end - a.ray_begin, cus);
-    if constexpr (NS >= 60) {  // STACK LDS entries, the rest of the worst case (bvh_depth) spills (NS >= 80 too)
+    if constexpr (NS % 200 >= 60) {  // STACK LDS entries, the rest of the worst case (bvh_depth) spills (NS >= 80 too)
         a.spill_depth = a.bvh_depth + 1 > STACK ? a.bvh_depth + 1 - STACK : 0;
         if (a.spill_depth > 0) {
             if (!a.spill) return hipErrorInvalidValue;
@@ -1927,6 +2161,29 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
         if ((uint64_t)grid > max_grid) grid = (int)max_grid;
         if (grid <= 0) return hipErrorInvalidValue;
     }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+// v5 launcher: direction pre-pass + static per-wave ranges; trees deeper than the LDS stack
+// take the spill-stack v3 kernel, quantized variants without a usable grid the f32 nodes.
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1>
+hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
+    if constexpr (NF >= 1) {
+        if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV>(args, cus, s);
+    }
+    if (args.bvh_depth + 1 > STACK) return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(args, cus, s);
+    TraceArgs a = args;
+    a.static_ranges = 1;
+    a.dirs = nullptr;
+    const uint64_t n_rays = a.ray_end - a.ray_begin;
+    if (a.dirs_buf && n_rays <= a.dirs_cap && n_rays > 0) {
+        const uint64_t g = (n_rays + 255) / 256;
+        hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)g), dim3(256), 0, s, a.seed, a.ray_begin, n_rays,
+                           reinterpret_cast<float4*>(a.dirs_buf));
+        a.dirs = a.dirs_buf;
+    }
+    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV>;
+    const int grid = persistent_grid(k, BLOCK, n_rays, cus);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
@@ -2144,6 +2401,40 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 859: return launch_v3<128, 12, 12, 12, 5, true, 1, 91, 3>(a, cus, s);  // instrumented
         case 863: return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(a, cus, s);  // default for deep trees
         case 749: return launch_v3<128, 12, 12, 28, 5, true, 1, 8, 3>(a, cus, s);  // instrumented
+        // 16-bit quantized 32-B nodes (NS = 200 + the f32 scheme)
+        case 900: return launch_v3<128, 12, 12, 28, 5, false, 1, 251, 3>(a, cus, s);
+        case 901: return launch_v3<128, 12, 12, 28, 5, false, 1, 271, 3>(a, cus, s);
+        case 902: return launch_v3<128, 12, 12, 28, 5, false, 1, 247, 3>(a, cus, s);
+        case 903: return launch_v3<128, 12, 12, 28, 5, false, 1, 255, 3>(a, cus, s);
+        case 904: return launch_v3<128, 16, 12, 28, 5, false, 1, 251, 3>(a, cus, s);
+        case 905: return launch_v3<128, 12, 12, 28, 6, false, 1, 251, 3>(a, cus, s);
+        case 906: return launch_v3<128, 12, 16, 28, 5, false, 1, 251, 3>(a, cus, s);
+        case 907: return launch_v3<128, 12, 12, 24, 6, false, 1, 271, 3>(a, cus, s);
+        case 908: return launch_v3<128, 12, 12, 20, 6, false, 1, 271, 3>(a, cus, s);
+        case 909: return launch_v3<128, 12, 12, 28, 5, true, 1, 251, 3>(a, cus, s);  // instrumented
+        // branch-minimal coded steps, pop at the end of a step (trace_kernel_v5)
+        case 920: return launch_v5<128, 28, 12, 12, 5, 12, 0>(a, cus, s);
+        case 921: return launch_v5<128, 28, 12, 12, 5, 12, 1>(a, cus, s);
+        case 922: return launch_v5<128, 28, 12, 12, 5, 8, 0>(a, cus, s);
+        case 923: return launch_v5<128, 28, 12, 12, 5, 16, 0>(a, cus, s);
+        case 924: return launch_v5<128, 28, 16, 12, 5, 12, 0>(a, cus, s);
+        case 925: return launch_v5<128, 28, 12, 8, 5, 12, 0>(a, cus, s);
+        case 926: return launch_v5<128, 28, 12, 16, 5, 12, 0>(a, cus, s);
+        case 927: return launch_v5<128, 28, 8, 12, 5, 12, 0>(a, cus, s);
+        case 928: return launch_v5<128, 28, 12, 12, 5, 6, 0>(a, cus, s);
+        case 929: return launch_v5<128, 28, 12, 12, 5, 16, 1>(a, cus, s);
+        case 930: return launch_v5<128, 25, 12, 12, 6, 12, 0>(a, cus, s);  // 6 waves/SIMD (trees <= 24 deep)
+        case 931: return launch_v5<128, 25, 12, 12, 6, 12, 1>(a, cus, s);
+        case 932: return launch_v5<128, 28, 12, 12, 5, 12, 2>(a, cus, s);  // octant copies of the quantized nodes
+        case 933: return launch_v5<128, 28, 12, 12, 5, 16, 2>(a, cus, s);
+        case 934: return launch_v5<128, 28, 16, 12, 5, 12, 2>(a, cus, s);
+        case 935: return launch_v5<128, 28, 12, 16, 5, 12, 2>(a, cus, s);
+        case 936: return launch_v5<128, 28, 12, 8, 5, 12, 2>(a, cus, s);
+        case 937: return launch_v5<128, 28, 8, 12, 5, 12, 2>(a, cus, s);
+        // 31-entry LDS stack (16 KB per 128-lane block: 10 blocks fill the 160 KB of LDS)
+        case 910: return launch_v3<128, 12, 12, 31, 5, false, 1, 251, 3>(a, cus, s);
+        case 911: return launch_v3<128, 12, 12, 31, 5, false, 1, 51, 3>(a, cus, s);
+        case 912: return launch_v3<128, 12, 12, 31, 5, false, 1, 271, 3>(a, cus, s);
         // wide trees (trace_width(): 300-309 -> 4-wide, 310-319 -> 8-wide)
         case 300: return launch_w<4, 128, 24, 32, 12, 5>(a, cus, s);
         case 301: return launch_w<4, 128, 32, 32, 12, 5>(a, cus, s);
@@ -2168,10 +2459,13 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 327: return launch_w<kWideQ4, 128, 24, 32, 24, 5>(a, cus, s);
         case 328: return launch_w<kWideQ4, 256, 24, 64, 12, 5>(a, cus, s);
         case 329: return launch_w<kWideQ4, 128, 28, 32, 12, 5>(a, cus, s);
-        default:  // = 772: static per-wave ray ranges, direction pre-pass, refill at 12 idle lanes,
-                  // coded nodes through a buffer resource, 12 node steps per inner iteration;
-                  // trees deeper than the 28-entry LDS stack spill to a global column (same
-                  // occupancy) instead of taking a bigger LDS stack
+        default:  // = 921: static per-wave ray ranges, direction pre-pass, refill at 12 idle lanes,
+                  // branch-free steps (trace_kernel_v5) over the 32-B quantized nodes, 12 per inner
+                  // iteration; launch_v5 takes the f32 coded nodes when the emitter is off the
+                  // quantization grid and the spill-stack v3 kernel (863) for trees deeper than
+                  // the 28-entry LDS stack
+            return launch_v5<128, 28, 12, 12, 5, 12, 1>(a, cus, s);
+        case 778:  // the round-1e default: 772, or 863 for trees deeper than its LDS stack
             if (a.bvh_depth < 28) return launch_v3<128, 12, 12, 28, 5, false, 1, 51, 3>(a, cus, s);
             return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(a, cus, s);
     }

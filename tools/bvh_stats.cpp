@@ -188,6 +188,10 @@ int main(int argc, char** argv) {
     if (const char* e = std::getenv("LEAF")) bp.leaf_max = std::atoi(e);
     if (const char* e = std::getenv("TRAV")) bp.trav_cost = (float)std::atof(e);
     if (const char* e = std::getenv("ISECT")) bp.isect_cost = (float)std::atof(e);
+    if (const char* e = std::getenv("SPATIAL")) bp.spatial = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ALPHA")) bp.spatial_alpha = (float)std::atof(e);
+    if (const char* e = std::getenv("SDEPTH")) bp.spatial_max_depth = std::atoi(e);
+    if (const char* e = std::getenv("BUDGET")) bp.spatial_budget = (float)std::atof(e);
     std::printf("params: bins %d leaf_max %d trav %.2f isect %.2f\n", bp.bins, bp.leaf_max, bp.trav_cost, bp.isect_cost);
     BvhBuild b;
     std::vector<float> ab(n, 0.5f);
@@ -207,6 +211,7 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> topq;
     make_wide_top(kWideQ4, wq.root, empty_child(), topq);
     Tree tq = from_q4(topq, wq);
+    std::printf("spatial %d alpha %g budget %g: refs %zu\n", (int)bp.spatial, bp.spatial_alpha, bp.spatial_budget, b.tris.size());
     std::printf("tris %ld  binary nodes %zu depth %d | wide4 %zu depth %d | wide8 %zu depth %d\n", n, b.nodes.size(),
                 b.depth, w4.count, w4.depth, w8.count, w8.depth);
     Tree* trees[4] = {&t2, &t4, &t8, &tq};
