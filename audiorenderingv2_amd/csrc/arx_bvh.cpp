@@ -1030,9 +1030,9 @@ bool quantize_nodes16(const BvhNode* coded, size_t n, const QGrid& g, QNode2* ou
                     ql = (uint32_t)l;
                     qh = (uint32_t)h;
                 }
-                out[i].q[3 * c + k] = ql | (qh << 16);
+                out[i].c[c].q[k] = ql | (qh << 16);
             }
-            out[i].code[c] = b.d[c];
+            out[i].c[c].code = b.d[c];
         }
     }
     return true;
@@ -1044,8 +1044,8 @@ void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out) {
         for (int c = 0; c < 2; ++c)
             for (int k = 0; k < 3; ++k)
                 if ((octant >> k) & 1) {
-                    const uint32_t w = q.q[3 * c + k];
-                    q.q[3 * c + k] = (w >> 16) | (w << 16);
+                    const uint32_t w = q.c[c].q[k];
+                    q.c[c].q[k] = (w >> 16) | (w << 16);
                 }
         out[i] = q;
     }

@@ -83,6 +83,9 @@ struct arx_renderer {
     QNode2* d_qnodes = nullptr;   // 16-bit quantized copies of d_cnodes: 8 octants x nodes_cap
     QGrid qgrid{};
     bool qgrid_set = false;
+    bool q_valid = false;         // d_qnodes (octant 0) matches the tree: the receiver is on the grid
+    bool qoct_valid = false;      // octants 1..7 too (uploaded only for the octant kernel variants)
+    std::vector<QNode2> qtop_h, qscene_h, qrecv_h;  // host images of the quantized parts
     size_t nodes_cap = 0;
     TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
@@ -270,12 +273,11 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
-    // quantized copy: a new grid (and a full re-quantization) when the scene changed or the
-    // receiver left the grid; the emitter is checked per launch (arx_trace_rays)
-    bool requant = full || !r->qgrid_set;
-    if (!requant && r->recv_dirty && r->recv.root.count >= 0 &&
-        !qgrid_contains(r->qgrid, r->recv.root.lo, r->recv.root.hi))
-        requant = true;
+    // quantized copy: a new grid (and a full re-quantization) only when the scene changed.  A
+    // receiver off the grid (a listener outside the room) or an emitter off it (checked per
+    // launch, arx_trace_rays) makes the launches take the f32 nodes until it is back: no
+    // re-quantization on the per-frame listener path
+    const bool requant = full || !r->qgrid_set;
     if (requant) {
         float lo[3], hi[3];
         for (int k = 0; k < 3; ++k) {
@@ -309,24 +311,11 @@ arx_status ensure_device_scene(arx_renderer* r) {
         code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
         ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-        QNode2 qtop;
-        std::vector<QNode2> qscene, qrecv(crecv.size());
-        if (!quantize_nodes16(&ctop, 1, r->qgrid, &qtop) ||
-            !quantize_nodes16(crecv.data(), crecv.size(), r->qgrid, qrecv.data()))
-            return fail(ARX_ERR_INTERNAL, "BVH quantization failed (box outside the grid)");
-        // the 8 octant copies of quantized nodes [at, at + n); host images live until the sync
-        std::vector<std::vector<QNode2>> qoct;
-        auto upload_q = [&](const QNode2* q, size_t n, size_t at) -> hipError_t {
-            hipError_t e = hipMemcpyAsync(r->d_qnodes + at, q, n * sizeof(QNode2), hipMemcpyHostToDevice, r->stream);
-            for (int o = 1; o < 8 && e == hipSuccess; ++o) {
-                qoct.emplace_back(n);
-                octant_nodes16(q, n, o, qoct.back().data());
-                e = hipMemcpyAsync(r->d_qnodes + (size_t)o * r->nodes_cap + at, qoct.back().data(), n * sizeof(QNode2),
-                                   hipMemcpyHostToDevice, r->stream);
-            }
-            return e;
-        };
-        ARX_HIP(upload_q(&qtop, 1, 0));
+        r->qtop_h.assign(1, QNode2{});
+        r->qrecv_h.assign(crecv.size(), QNode2{});
+        const bool q_ok = quantize_nodes16(&ctop, 1, r->qgrid, r->qtop_h.data()) &&
+                          quantize_nodes16(crecv.data(), crecv.size(), r->qgrid, r->qrecv_h.data());
+        if (q_ok) ARX_HIP(hipMemcpyAsync(r->d_qnodes, r->qtop_h.data(), sizeof(QNode2), hipMemcpyHostToDevice, r->stream));
         if ((full || requant) && !r->scene.nodes.empty()) {
             cscene.resize(r->scene.nodes.size());
             code_nodes(r->scene.nodes.data(), r->scene.nodes.size(), cscene.data());
@@ -336,10 +325,13 @@ arx_status ensure_device_scene(arx_renderer* r) {
                 ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
                                        hipMemcpyHostToDevice, r->stream));
             }
-            qscene.resize(cscene.size());
-            if (!quantize_nodes16(cscene.data(), cscene.size(), r->qgrid, qscene.data()))
+            r->qscene_h.assign(cscene.size(), QNode2{});
+            if (!quantize_nodes16(cscene.data(), cscene.size(), r->qgrid, r->qscene_h.data()))
                 return fail(ARX_ERR_INTERNAL, "BVH quantization failed (scene box outside the grid)");
-            ARX_HIP(upload_q(qscene.data(), qscene.size(), 1));
+            ARX_HIP(hipMemcpyAsync(r->d_qnodes + 1, r->qscene_h.data(), r->qscene_h.size() * sizeof(QNode2),
+                                   hipMemcpyHostToDevice, r->stream));
+        } else if (full || requant) {
+            r->qscene_h.clear();
         }
         if (full && !r->scene.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
@@ -349,13 +341,36 @@ arx_status ensure_device_scene(arx_renderer* r) {
                                    r->recv.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
             ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
                                    crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-            ARX_HIP(upload_q(qrecv.data(), qrecv.size(), 1 + r->scene.nodes.size()));
+            if (q_ok)
+                ARX_HIP(hipMemcpyAsync(r->d_qnodes + 1 + r->scene.nodes.size(), r->qrecv_h.data(),
+                                       r->qrecv_h.size() * sizeof(QNode2), hipMemcpyHostToDevice, r->stream));
         }
         if (!r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
                                    r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
+        r->q_valid = q_ok;
+        r->qoct_valid = false;
         // the host vectors are pageable: make sure the copies are done before they can change
         ARX_HIP(hipStreamSynchronize(r->stream));
+    }
+    if (trace_octant_nodes() && r->q_valid && !r->qoct_valid) {
+        // octant copies 1..7 of the whole quantized tree (octant 0 is the plain copy)
+        std::vector<QNode2> img;
+        auto put = [&](const std::vector<QNode2>& q, size_t at, int o) -> hipError_t {
+            if (q.empty()) return hipSuccess;
+            img.resize(q.size());
+            octant_nodes16(q.data(), q.size(), o, img.data());
+            hipError_t e = hipMemcpyAsync(r->d_qnodes + (size_t)o * r->nodes_cap + at, img.data(),
+                                          q.size() * sizeof(QNode2), hipMemcpyHostToDevice, r->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(r->stream);  // img is reused
+            return e;
+        };
+        for (int o = 1; o < 8; ++o) {
+            ARX_HIP(put(r->qtop_h, 0, o));
+            ARX_HIP(put(r->qscene_h, 1, o));
+            ARX_HIP(put(r->qrecv_h, 1 + r->scene.nodes.size(), o));
+        }
+        r->qoct_valid = true;
     }
     arx_status st = ensure_wide(r, scene_changed || full, recv_changed);
     if (st != ARX_OK) return st;
@@ -615,7 +630,8 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         // quantized nodes only while the emitter (the one ray origin off the geometry) is on the
         // grid: the slab arithmetic's error bound assumes origins within the grid's extent
         const float* e = r->emitter;
-        a.qnodes = (r->qgrid_set && qgrid_contains(r->qgrid, e, e)) ? r->d_qnodes : nullptr;
+        const bool oct_ok = !trace_octant_nodes() || r->qoct_valid;
+        a.qnodes = (r->q_valid && oct_ok && qgrid_contains(r->qgrid, e, e)) ? r->d_qnodes : nullptr;
         a.qgrid = r->qgrid;
         a.qostride = (uint32_t)r->nodes_cap;
     }

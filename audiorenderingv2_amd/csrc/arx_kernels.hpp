@@ -14,6 +14,8 @@ int trace_grid_size(uint64_t n_rays, int device_cus);
 // cus = compute units of the device (grid sizing); the variant comes from ARX_TRACE_KERNEL.
 hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s);
 int trace_variant();
+// True for the variants that read the octant copies of the quantized nodes (TraceArgs::qnodes).
+bool trace_octant_nodes();
 // Node width the current variant traverses: 2 (BvhNode) or 4 / 8 (WideNode<W>, a.wnodes).
 int trace_width();
 // Upper bound on the lanes a persistent wide-tree launch uses (spill buffer columns).

@@ -72,10 +72,14 @@ constexpr int kWideQ4 = 5;
 // coded node (code_nodes) with both child boxes on one scene-wide 16-bit grid per axis,
 // plane = grid.origin + q * grid.scale (real arithmetic), rounded outward with a 0.1-step margin so
 // the kernel's f32 slab arithmetic stays conservative (quantize_nodes16, arx_bvh.cpp).
-//   q[0..2] = child 0 x, y, z as (lo | hi << 16); q[3..5] = child 1; code[2] as in code_nodes.
+// Each 16-B half is one child: q[0..2] = x, y, z as (lo | hi << 16), code as in code_nodes, so
+// a lane pair can fetch a node with one 16-B load each (node_step8p).
+struct QChild {
+    uint32_t q[3];
+    int32_t code;
+};
 struct alignas(16) QNode2 {
-    uint32_t q[6];
-    int32_t code[2];
+    QChild c[2];
 };
 static_assert(sizeof(QNode2) == 32, "QNode2 must be 32 B");
 

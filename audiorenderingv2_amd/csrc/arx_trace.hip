@@ -146,12 +146,15 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
     r.op[0] = sel3(o.x, o.y, o.z, kx);
     r.op[1] = sel3(o.x, o.y, o.z, ky);
     r.op[2] = sel3(o.x, o.y, o.z, kz);
+    // Box-test reciprocals: v_rcp_f32 (1 ulp) instead of a correctly rounded division -- the
+    // slab test only has to be conservative, and a 1e-7 relative error in t is far inside the
+    // 1e-5 * max|coordinate| box padding; the closest hit comes from the exact triangle test.
     const float dd[3] = {d.x, d.y, d.z};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         float v = dd[k];
         if (fabsf(v) < 1e-20f) v = (v < 0.0f) ? -1e-20f : 1e-20f;
-        r.inv[k] = 1.0f / v;
+        r.inv[k] = __builtin_amdgcn_rcpf(v);
     }
 }
 
@@ -792,9 +795,9 @@ __device__ __forceinline__ void node_step7(const TraceArgs& a, const Ray& r, flo
         // same register roles as the f32 node: na = (x0 lo, x0 hi, y0 lo, y0 hi), nb = child 1,
         // nc = (z0 lo, z0 hi, z1 lo, z1 hi)
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
-        nb = make_float4((float)(A.w & 0xffffu), (float)(A.w >> 16), (float)(B.x & 0xffffu), (float)(B.x >> 16));
-        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
-        nd = make_int2((int)B.z, (int)B.w);
+        nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
+        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
+        nd = make_int2((int)A.w, (int)B.w);
     } else if constexpr (BUF) {
         const int off = t.node * (int)sizeof(BvhNode);
         na = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -1538,18 +1541,18 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
         const int off = obase + t.node * (int)sizeof(QNode2);
         const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
-        // child 0: A.x, A.y, A.z; child 1: A.w, B.x, B.y (x, y, z words)
+        // child 0: A.x, A.y, A.z; child 1: B.x, B.y, B.z (x, y, z words)
         const float nx0 = __builtin_fmaf((float)(A.x & 0xffffu), ix, -oix), fx0 = __builtin_fmaf((float)(A.x >> 16), ix, -oix);
         const float ny0 = __builtin_fmaf((float)(A.y & 0xffffu), iy, -oiy), fy0 = __builtin_fmaf((float)(A.y >> 16), iy, -oiy);
         const float nz0 = __builtin_fmaf((float)(A.z & 0xffffu), iz, -oiz), fz0 = __builtin_fmaf((float)(A.z >> 16), iz, -oiz);
-        const float nx1 = __builtin_fmaf((float)(A.w & 0xffffu), ix, -oix), fx1 = __builtin_fmaf((float)(A.w >> 16), ix, -oix);
-        const float ny1 = __builtin_fmaf((float)(B.x & 0xffffu), iy, -oiy), fy1 = __builtin_fmaf((float)(B.x >> 16), iy, -oiy);
-        const float nz1 = __builtin_fmaf((float)(B.y & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(B.y >> 16), iz, -oiz);
+        const float nx1 = __builtin_fmaf((float)(B.x & 0xffffu), ix, -oix), fx1 = __builtin_fmaf((float)(B.x >> 16), ix, -oix);
+        const float ny1 = __builtin_fmaf((float)(B.y & 0xffffu), iy, -oiy), fy1 = __builtin_fmaf((float)(B.y >> 16), iy, -oiy);
+        const float nz1 = __builtin_fmaf((float)(B.z & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(B.z >> 16), iz, -oiz);
         tn0 = fmaxf(fmaxf(nx0, ny0), fmaxf(nz0, 0.0f));
         tf0 = fminf(fminf(fx0, fy0), fminf(fz0, t.best_t));
         tn1 = fmaxf(fmaxf(nx1, ny1), fmaxf(nz1, 0.0f));
         tf1 = fminf(fminf(fx1, fy1), fminf(fz1, t.best_t));
-        c0 = (int)B.z;
+        c0 = (int)A.w;
         c1 = (int)B.w;
     } else {
     float4 na, nb, nc;
@@ -1558,9 +1561,9 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
         const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
-        nb = make_float4((float)(A.w & 0xffffu), (float)(A.w >> 16), (float)(B.x & 0xffffu), (float)(B.x >> 16));
-        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
-        c0 = (int)B.z;
+        nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
+        nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
+        c0 = (int)A.w;
         c1 = (int)B.w;
     } else {  // coded BvhNode, 56 B
         const int off = t.node * (int)sizeof(BvhNode);
@@ -1598,6 +1601,61 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
     const int popped = sp > 0 ? top : -1;
     t.node = any ? c_near : popped;
     t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
+}
+
+// NF 3: pair-cooperative fetch of QNode2 nodes.  The vector-memory data path is charged per
+// distinct 64-B block per wave-instruction (td_microbench), and two per-lane 16-B loads of a
+// 32-B node touch 2 x 64 blocks per step.  Here lane pair (2p, 2p+1) fetches its two nodes
+// together: load 0 brings each lane its own node's child (lane & 1), load 1 the partner node's
+// child (lane & 1) -- the half the partner is missing -- and one DPP swap hands it over, so
+// each load touches 32 blocks.  The two children are then tested symmetrically ("mine" = the
+// child this lane loaded, "other" = the swapped one; their codes travel with them), so the
+// order of a tie between equally near children depends on the lane's parity: the closest hit,
+// a minimum over every triangle not culled, does not.  Runs with the whole wave active (the
+// partner may need this lane's load); lanes without a step (go false) fetch node 0 and keep
+// their state.
+__device__ __forceinline__ int swap_pair(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+
+template <int BLOCK, int STACK>
+__device__ __forceinline__ void node_step8p(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                            int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs, bool go,
+                                            int half) {
+    const int me = max(t.node, 0);
+    const int pn = swap_pair(me);
+    const uint4 D0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, me * (int)sizeof(QNode2) + half, 0, 0));
+    const uint4 D1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, pn * (int)sizeof(QNode2) + half, 0, 0));
+    uint4 Y;
+    Y.x = (uint32_t)swap_pair((int)D1.x);
+    Y.y = (uint32_t)swap_pair((int)D1.y);
+    Y.z = (uint32_t)swap_pair((int)D1.z);
+    Y.w = (uint32_t)swap_pair((int)D1.w);
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float xa0 = __builtin_fmaf((float)(D0.x & 0xffffu), ix, -oix), xa1 = __builtin_fmaf((float)(D0.x >> 16), ix, -oix);
+    const float ya0 = __builtin_fmaf((float)(D0.y & 0xffffu), iy, -oiy), ya1 = __builtin_fmaf((float)(D0.y >> 16), iy, -oiy);
+    const float za0 = __builtin_fmaf((float)(D0.z & 0xffffu), iz, -oiz), za1 = __builtin_fmaf((float)(D0.z >> 16), iz, -oiz);
+    const float xb0 = __builtin_fmaf((float)(Y.x & 0xffffu), ix, -oix), xb1 = __builtin_fmaf((float)(Y.x >> 16), ix, -oix);
+    const float yb0 = __builtin_fmaf((float)(Y.y & 0xffffu), iy, -oiy), yb1 = __builtin_fmaf((float)(Y.y >> 16), iy, -oiy);
+    const float zb0 = __builtin_fmaf((float)(Y.z & 0xffffu), iz, -oiz), zb1 = __builtin_fmaf((float)(Y.z >> 16), iz, -oiz);
+    const float tna = fmaxf(fmaxf(fminf(xa0, xa1), fminf(ya0, ya1)), fmaxf(fminf(za0, za1), 0.0f));
+    const float tfa = fminf(fminf(fmaxf(xa0, xa1), fmaxf(ya0, ya1)), fminf(fmaxf(za0, za1), t.best_t));
+    const float tnb = fmaxf(fmaxf(fminf(xb0, xb1), fminf(yb0, yb1)), fmaxf(fminf(zb0, zb1), 0.0f));
+    const float tfb = fminf(fminf(fmaxf(xb0, xb1), fmaxf(yb0, yb1)), fminf(fmaxf(zb0, zb1), t.best_t));
+    const int ca = (int)D0.w, cb = (int)Y.w;
+    const bool ha = go & (tna <= tfa), hb = go & (tnb <= tfb);
+    const bool nearb = hb & (!ha | (tnb < tna));
+    const int c_near = nearb ? cb : ca;
+    const int c_far = nearb ? ca : cb;
+    const int sp = t.sp;
+    stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
+    asm volatile("" : "+v"(top));
+    const bool any = ha | hb;
+    const int popped = sp > 0 ? top : -1;
+    const int nn = any ? c_near : popped;
+    const int ns = any ? sp + (int)(ha & hb) : sp_pop;
+    t.node = go ? nn : t.node;
+    t.sp = go ? ns : t.sp;
 }
 
 // Leaf phase of v5: test the pending leaf, then pop the next entry.
@@ -1704,9 +1762,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             if ((m_node | m_leaf) == 0ull) break;
             if (__popcll(__ballot(active && !trav)) >= THRESH) break;
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+                if constexpr (NF == 3) {  // whole-wave steps (pair-cooperative fetch)
+                    const int half = (lane & 1) * (int)sizeof(QChild);
 #pragma unroll
-                for (int k = 0; k < NSTEPS; ++k)
-                    if (t.node >= 0) node_step8<BLOCK, STACK, NF>(r, oix, oiy, oiz, t, stk, lane, nrs, obase);
+                    for (int k = 0; k < NSTEPS; ++k) {
+                        const bool go = t.node >= 0;
+                        if (__ballot(go) == 0ull) break;
+                        node_step8p<BLOCK, STACK>(r, oix, oiy, oiz, t, stk, lane, nrs, go, half);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NSTEPS; ++k)
+                        if (t.node >= 0) node_step8<BLOCK, STACK, NF>(r, oix, oiy, oiz, t, stk, lane, nrs, obase);
+                }
             } else if (t.node <= -2) {
                 leaf_step8<BLOCK, LV>(a, r, t, stk, lane);
             }
@@ -2197,6 +2265,11 @@ int trace_width() {
     return 2;
 }
 
+bool trace_octant_nodes() {
+    const int v = trace_variant();
+    return v >= 932 && v <= 937;
+}
+
 int trace_variant() {
     const char* v = getenv("ARX_TRACE_KERNEL");
     return (v && v[0]) ? atoi(v) : kDefaultVariant;
@@ -2425,6 +2498,12 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 929: return launch_v5<128, 28, 12, 12, 5, 16, 1>(a, cus, s);
         case 930: return launch_v5<128, 25, 12, 12, 6, 12, 0>(a, cus, s);  // 6 waves/SIMD (trees <= 24 deep)
         case 931: return launch_v5<128, 25, 12, 12, 6, 12, 1>(a, cus, s);
+        case 940: return launch_v5<128, 28, 12, 12, 5, 12, 3>(a, cus, s);  // pair-cooperative fetch
+        case 941: return launch_v5<128, 28, 12, 12, 5, 16, 3>(a, cus, s);
+        case 942: return launch_v5<128, 28, 12, 12, 5, 8, 3>(a, cus, s);
+        case 943: return launch_v5<128, 28, 16, 12, 5, 12, 3>(a, cus, s);
+        case 944: return launch_v5<128, 28, 12, 16, 5, 12, 3>(a, cus, s);
+        case 945: return launch_v5<128, 28, 12, 8, 5, 12, 3>(a, cus, s);
         case 932: return launch_v5<128, 28, 12, 12, 5, 12, 2>(a, cus, s);  // octant copies of the quantized nodes
         case 933: return launch_v5<128, 28, 12, 12, 5, 16, 2>(a, cus, s);
         case 934: return launch_v5<128, 28, 16, 12, 5, 12, 2>(a, cus, s);
