@@ -1534,6 +1534,11 @@ template <int BLOCK, int STACK, int NF>
 __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
                                            int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs,
                                            int obase = 0) {
+    // the pop candidate is read first, so its LDS latency hides under the node fetch (the
+    // slot sp - 1 is not touched by this step's write to slot sp)
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
     float tn0, tf0, tn1, tf1;
     int c0, c1;
@@ -1592,10 +1597,7 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
     const int c_far = near1 ? c0 : c1;
     // The stack never overflows: it holds at most one entry per tree level and the launcher
     // requires STACK > bvh_depth.  The clamp only keeps the write inside the array.
-    const int sp = t.sp;
     stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
-    const int sp_pop = max(sp - 1, 0);
-    int top = stk[sp_pop * BLOCK + lane];
     asm volatile("" : "+v"(top));  // the pop read stays unconditional (no branch around it)
     const bool any = h0 | h1;
     const int popped = sp > 0 ? top : -1;
@@ -1620,6 +1622,9 @@ template <int BLOCK, int STACK>
 __device__ __forceinline__ void node_step8p(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
                                             int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs, bool go,
                                             int half) {
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];  // pop candidate first (see node_step8)
     const int me = max(t.node, 0);
     const int pn = swap_pair(me);
     const uint4 D0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, me * (int)sizeof(QNode2) + half, 0, 0));
@@ -1645,10 +1650,7 @@ __device__ __forceinline__ void node_step8p(const Ray& r, float oix, float oiy, 
     const bool nearb = hb & (!ha | (tnb < tna));
     const int c_near = nearb ? cb : ca;
     const int c_far = nearb ? ca : cb;
-    const int sp = t.sp;
     stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
-    const int sp_pop = max(sp - 1, 0);
-    int top = stk[sp_pop * BLOCK + lane];
     asm volatile("" : "+v"(top));
     const bool any = ha | hb;
     const int popped = sp > 0 ? top : -1;
