@@ -2500,6 +2500,17 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 929: return launch_v5<128, 28, 12, 12, 5, 16, 1>(a, cus, s);
         case 930: return launch_v5<128, 25, 12, 12, 6, 12, 0>(a, cus, s);  // 6 waves/SIMD (trees <= 24 deep)
         case 931: return launch_v5<128, 25, 12, 12, 6, 12, 1>(a, cus, s);
+        // tunings of the default (921)
+        case 950: return launch_v5<128, 28, 8, 12, 5, 12, 1>(a, cus, s);
+        case 951: return launch_v5<128, 28, 16, 12, 5, 12, 1>(a, cus, s);
+        case 952: return launch_v5<128, 28, 12, 8, 5, 12, 1>(a, cus, s);
+        case 953: return launch_v5<128, 28, 12, 16, 5, 12, 1>(a, cus, s);
+        case 954: return launch_v5<128, 28, 12, 12, 5, 12, 1, 2>(a, cus, s);
+        case 955: return launch_v5<128, 28, 12, 12, 5, 10, 1>(a, cus, s);
+        case 956: return launch_v5<128, 28, 12, 12, 5, 14, 1>(a, cus, s);
+        case 957: return launch_v5<64, 28, 12, 12, 5, 12, 1>(a, cus, s);
+        case 958: return launch_v5<128, 28, 10, 10, 5, 12, 1>(a, cus, s);
+        case 959: return launch_v5<128, 28, 14, 14, 5, 12, 1>(a, cus, s);
         case 940: return launch_v5<128, 28, 12, 12, 5, 12, 3>(a, cus, s);  // pair-cooperative fetch
         case 941: return launch_v5<128, 28, 12, 12, 5, 16, 3>(a, cus, s);
         case 942: return launch_v5<128, 28, 12, 12, 5, 8, 3>(a, cus, s);
