@@ -1676,7 +1676,10 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 
 // Persistent waves as v3 (static per-wave ray ranges, direction pre-pass, refill at THRESH
 // idle lanes, postponed leaves) over node_step8: NSTEPS guarded steps per inner iteration.
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1>
+// POOL > 0: the last POOL percent of the rays form a shared pool that waves done with their
+// static range take from in refill-sized pieces (one atomic per refill, only near the end), so
+// waves whose rays ran long do not hold the launch open while others idle.
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     constexpr bool Q16 = NF >= 1;
     __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: target of writes past a full stack
@@ -1685,13 +1688,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             : node_rsrc(a.cnodes);
     const int lane = threadIdx.x;
     const uint64_t n = a.ray_end - a.ray_begin;
+    const uint64_t n_static = POOL > 0 ? n - n * (uint64_t)POOL / 100 : n;  // [n_static, n): the pool
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint64_t w_next = n * wave_id / n_waves;
-    const uint64_t w_end = n * (wave_id + 1) / n_waves;
+    uint64_t w_next = n_static * wave_id / n_waves;
+    uint64_t w_end = n_static * (wave_id + 1) / n_waves;
+    bool pool = false;  // this wave has moved on to the shared pool
+    unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
     const bool overflow = false;  // impossible by construction (node_step8)
-    bool active = false, trav = false, exhausted = w_next >= w_end;
+    bool active = false, trav = false, exhausted = POOL > 0 ? false : w_next >= w_end;
     RayState s;
     s.depth = -1;
     Ray r;
@@ -1714,8 +1720,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
         const unsigned long long need = __ballot(!active);
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
-            const uint64_t base = w_next;
-            w_next += (uint64_t)cnt;
+            if (POOL > 0 && !pool && w_next >= w_end) pool = true;
+            uint64_t base = w_next;
+            if (POOL > 0 && pool) {  // one atomic per refill, wave-uniform result
+                const int leader = __ffsll((unsigned long long)need) - 1;
+                unsigned long long got = 0;
+                if ((lane & 63) == leader) got = atomicAdd(cursor, (unsigned long long)cnt);
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)got, leader);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(got >> 32), leader);
+                base = n_static + (((uint64_t)hi << 32) | lo);
+                w_end = n;
+            } else {
+                w_next += (uint64_t)cnt;
+            }
             if (!active) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -1725,7 +1742,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
                     active = wants_query(a, s);
                 }
             }
-            if (base + (uint64_t)cnt >= w_end) exhausted = true;
+            if (base + (uint64_t)cnt >= w_end && (POOL == 0 || pool)) exhausted = true;
         }
         if (active && !trav) {
             ++n_q;
@@ -2236,10 +2253,10 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
 }
 // v5 launcher: direction pre-pass + static per-wave ranges; trees deeper than the LDS stack
 // take the spill-stack v3 kernel, quantized variants without a usable grid the f32 nodes.
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1>
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
 hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
     if constexpr (NF >= 1) {
-        if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV>(args, cus, s);
+        if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV, POOL>(args, cus, s);
     }
     if (args.bvh_depth + 1 > STACK) return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(args, cus, s);
     TraceArgs a = args;
@@ -2252,7 +2269,11 @@ hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
                            reinterpret_cast<float4*>(a.dirs_buf));
         a.dirs = a.dirs_buf;
     }
-    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV>;
+    if constexpr (POOL > 0) {
+        const hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // pool cursor
+        if (e != hipSuccess) return e;
+    }
+    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL>;
     const int grid = persistent_grid(k, BLOCK, n_rays, cus);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
@@ -2500,6 +2521,12 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 929: return launch_v5<128, 28, 12, 12, 5, 16, 1>(a, cus, s);
         case 930: return launch_v5<128, 25, 12, 12, 6, 12, 0>(a, cus, s);  // 6 waves/SIMD (trees <= 24 deep)
         case 931: return launch_v5<128, 25, 12, 12, 6, 12, 1>(a, cus, s);
+        // static ranges + a shared pool of the last POOL % of the rays
+        case 960: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 5>(a, cus, s);
+        case 961: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 10>(a, cus, s);
+        case 962: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 25>(a, cus, s);
+        case 963: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 50>(a, cus, s);
+        case 964: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 100>(a, cus, s);
         // tunings of the default (921)
         case 950: return launch_v5<128, 28, 8, 12, 5, 12, 1>(a, cus, s);
         case 951: return launch_v5<128, 28, 16, 12, 5, 12, 1>(a, cus, s);
