@@ -1597,7 +1597,7 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
     const int c_far = near1 ? c0 : c1;
     // The stack never overflows: it holds at most one entry per tree level and the launcher
     // requires STACK > bvh_depth.  The clamp only keeps the write inside the array.
-    stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
+    stk[min(sp, STACK - 1) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
     asm volatile("" : "+v"(top));  // the pop read stays unconditional (no branch around it)
     const bool any = h0 | h1;
     const int popped = sp > 0 ? top : -1;
@@ -1650,7 +1650,7 @@ __device__ __forceinline__ void node_step8p(const Ray& r, float oix, float oiy, 
     const bool nearb = hb & (!ha | (tnb < tna));
     const int c_near = nearb ? cb : ca;
     const int c_far = nearb ? ca : cb;
-    stk[min(sp, STACK) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
+    stk[min(sp, STACK - 1) * BLOCK + lane] = c_far;  // above the top of the stack unless pushed
     asm volatile("" : "+v"(top));
     const bool any = ha | hb;
     const int popped = sp > 0 ? top : -1;
@@ -1682,7 +1682,9 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     constexpr bool Q16 = NF >= 1;
-    __shared__ int stk[(STACK + 1) * BLOCK];  // row STACK: target of writes past a full stack
+    // STACK rows: sp <= bvh_depth < STACK (launch_v5), so the unconditional write to slot sp
+    // stays in the array
+    __shared__ int stk[STACK * BLOCK];
     const __amdgpu_buffer_rsrc_t nrs =
         Q16 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
             : node_rsrc(a.cnodes);
@@ -2521,6 +2523,9 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 929: return launch_v5<128, 28, 12, 12, 5, 16, 1>(a, cus, s);
         case 930: return launch_v5<128, 25, 12, 12, 6, 12, 0>(a, cus, s);  // 6 waves/SIMD (trees <= 24 deep)
         case 931: return launch_v5<128, 25, 12, 12, 6, 12, 1>(a, cus, s);
+        // 6 waves per SIMD: 26-entry stack (13.3 KB per block; trees up to 25 levels)
+        case 970: return launch_v5<128, 26, 12, 12, 6, 12, 1>(a, cus, s);
+        case 971: return launch_v5<128, 26, 12, 12, 6, 8, 1>(a, cus, s);
         // static ranges + a shared pool of the last POOL % of the rays
         case 960: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 5>(a, cus, s);
         case 961: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 10>(a, cus, s);

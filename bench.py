@@ -38,6 +38,10 @@ WORKLOADS = {
     "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, frames=128000,
                desc="configs[1]: conference stand-in, 100K rays x 8 bounces per GPU, 16 kHz IR, "
                     "convolution of 128000 frames (experimento_entrada_16KHz length) per GPU"),
+    # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the ranks (strong)
+    "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, frames=807498, total=True,
+               desc="configs[3]: conference stand-in, 10M rays x 32 bounces in total, ray-sharded across the "
+                    "ranks, 48 kHz IR, RCCL IR all-reduce; convolution of 807498 frames per GPU"),
 }
 
 
@@ -177,9 +181,15 @@ def main(argv=None) -> int:
     dev = torch.device("cuda", local)
     wl = WORKLOADS[args.workload]
     rx, ry, rz = wl["rays"]
-    rays_per_gpu = rx * ry * rz
-    total_rays = rays_per_gpu * world
-    settings = RenderSettings(rays=(rx * world, ry, rz), ir_length_in_seconds=2, sample_rate=wl["sample_rate"],
+    if wl.get("total"):  # a fixed total split over the ranks (strong scaling)
+        total_rays = rx * ry * rz
+        rays_per_gpu = total_rays // world
+        launch = (rx, ry, rz)
+    else:  # a fixed shard per rank (weak scaling)
+        rays_per_gpu = rx * ry * rz
+        total_rays = rays_per_gpu * world
+        launch = (rx * world, ry, rz)
+    settings = RenderSettings(rays=launch, ir_length_in_seconds=2, sample_rate=wl["sample_rate"],
                               base_power=3.62, max_bounces=wl["max_bounces"], hrtf_absorption_rate=1.0, seed=1,
                               device=local)
     scene = conference_standin()
@@ -256,7 +266,7 @@ def main(argv=None) -> int:
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if wl.get("total") else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: deterministic conference.obj stand-in (seed 42; conference.obj is missing from the "
