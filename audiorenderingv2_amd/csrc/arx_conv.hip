@@ -175,6 +175,10 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
     const int n2_0 = blockIdx.x * tc;
     const int n2 = n2_0 + col;
     double2* buf = lds + (size_t)col * a.N1;
+    // the N1 twiddles W_N1^e, staged once in LDS after the columns (a global load per
+    // butterfly put an L2 round trip into every FFT stage)
+    double2* twl = lds + (size_t)tc * a.N1;
+    for (int i = threadIdx.x; i < a.N1; i += kThreads) twl[i] = a.tw[(size_t)i * (a.M / a.N1)];
     // load column n2: element n1 at x[N2*n1 + n2]
     for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
         const int c = i % tc, n1 = i / tc;  // consecutive threads -> consecutive columns
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
         lds[(size_t)c * a.N1 + n1] = x;
     }
     __syncthreads();
-    lds_fft(buf, a.N1, a.lg1, -1, t, per, a.tw, a.M);
+    lds_fft(buf, a.N1, a.lg1, -1, t, per, twl, a.N1);
     // twiddle W_M^(n2*k1) and store transposed: S[k1*N2 + n2]
     double2* dst = (MODE != 1) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
     for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
@@ -214,9 +218,13 @@ __global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
     const int64_t batch = blockIdx.y;
     const int N2 = a.N2;
     double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
-    for (int i = threadIdx.x; i < N2; i += kThreads) lds[i] = row[i];
+    double2* twl = lds + N2;  // W_N2^e staged in LDS (see pass A)
+    for (int i = threadIdx.x; i < N2; i += kThreads) {
+        lds[i] = row[i];
+        twl[i] = a.tw[(size_t)i * (a.M / N2)];
+    }
     __syncthreads();
-    lds_fft(lds, N2, a.lg2, -1, threadIdx.x, kThreads, a.tw, a.M);
+    lds_fft(lds, N2, a.lg2, -1, threadIdx.x, kThreads, twl, N2);
     if (MODE == 1) {
         for (int i = threadIdx.x; i < N2; i += kThreads) row[i] = lds[i];
         return;
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
             if (i < N2) lds[i] = cmul(keep[b], Hc[i]);
         }
         __syncthreads();
-        lds_fft(lds, N2, a.lg2, +1, threadIdx.x, kThreads, a.tw, a.M);
+        lds_fft(lds, N2, a.lg2, +1, threadIdx.x, kThreads, twl, N2);
         double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
         for (int i = threadIdx.x; i < N2; i += kThreads)
             dst[i] = cmul(lds[i], twiddle(a.tw, a.M, (int64_t)i * k1, +1));
@@ -256,12 +264,14 @@ __global__ __launch_bounds__(kThreads) void pass_c(PassArgs a) {
     const int ch = blockIdx.y & 1;
     const int n2_0 = blockIdx.x * tc;
     const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
+    double2* twl = lds + (size_t)tc * a.N1;  // W_N1^e staged in LDS (see pass A)
+    for (int i = threadIdx.x; i < a.N1; i += kThreads) twl[i] = a.tw[(size_t)i * (a.M / a.N1)];
     for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
         const int c = i % tc, k1 = i / tc;
         lds[(size_t)c * a.N1 + k1] = src[(int64_t)k1 * a.N2 + n2_0 + c];
     }
     __syncthreads();
-    lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, a.tw, a.M);
+    lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, twl, a.N1);
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
     double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
     double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
@@ -388,8 +398,8 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     PassArgs a = base_args(p);
     a.ir_l = d_ir_left;
     a.ir_r = d_ir_right;
-    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
-    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
+    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_b<1>, dim3(p->N1, 2), dim3(kThreads), lds_b, s, a);
     return hipGetLastError();
@@ -428,8 +438,8 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.out_l = d_out_left;
     a.out_r = d_out_right;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
-    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
-    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
+    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
@@ -462,8 +472,8 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.n_pairs = 1;
     a.out_d = d_out_interleaved;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
-    const size_t lds_a = (size_t)p->tc * p->N1 * sizeof(double2);
-    const size_t lds_b = (size_t)p->N2 * sizeof(double2);
+    const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
+    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, 1), dim3(kThreads), lds_b, s, a);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
