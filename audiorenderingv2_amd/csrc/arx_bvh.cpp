@@ -974,10 +974,10 @@ void code_nodes(const BvhNode* in, size_t n, BvhNode* out) {
     }
 }
 
-QGrid make_qgrid(const float lo[3], const float hi[3]) {
+QGrid make_qgrid(const float lo[3], const float hi[3], double margin_frac) {
     double ext = 0.0;
     for (int k = 0; k < 3; ++k) ext = std::max(ext, (double)hi[k] - (double)lo[k]);
-    const double margin = std::max(0.1 * ext, 1e-2);
+    const double margin = std::max(margin_frac * ext, 1e-2);
     QGrid g;
     for (int k = 0; k < 3; ++k) {
         const double o = (double)lo[k] - margin;

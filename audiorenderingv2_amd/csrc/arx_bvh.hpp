@@ -67,8 +67,9 @@ bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size
 constexpr int32_t kEmptyChildCode = ~16;
 void code_nodes(const BvhNode* in, size_t n, BvhNode* out);
 // Grid for QNode2 trees covering the box [lo, hi] (scene, receiver and emitter) with a margin
-// of 1/10 of the largest extent on every side, so listener moves inside the room keep the grid.
-QGrid make_qgrid(const float lo[3], const float hi[3]);
+// of margin_frac of the largest extent on every side, so listener moves inside the room keep
+// the grid.
+QGrid make_qgrid(const float lo[3], const float hi[3], double margin_frac = 0.1);
 // True if the box [lo, hi] lies inside the grid with room for the outward rounding.
 bool qgrid_contains(const QGrid& g, const float lo[3], const float hi[3]);
 // Quantized copy of coded nodes: every child box is rounded outward to the grid with a margin of

@@ -273,11 +273,14 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
-    // quantized copy: a new grid (and a full re-quantization) only when the scene changed.  A
-    // receiver off the grid (a listener outside the room) or an emitter off it (checked per
-    // launch, arx_trace_rays) makes the launches take the f32 nodes until it is back: no
-    // re-quantization on the per-frame listener path
-    const bool requant = full || !r->qgrid_set;
+    // quantized copy: a new grid (and a full re-quantization) when the scene changed, or once
+    // when the receiver first leaves the grid (a listener walking out of the room): the new
+    // grid spans the old one, the scene, the receiver and the emitter with half the extent as
+    // margin, so such a walk re-grids once or twice, not per frame.  An emitter off the grid
+    // (checked per launch, arx_trace_rays) makes the launches take the f32 nodes instead.
+    const bool grow = !full && r->qgrid_set && r->recv_dirty && r->recv.root.count >= 0 &&
+                      !qgrid_contains(r->qgrid, r->recv.root.lo, r->recv.root.hi);
+    const bool requant = full || !r->qgrid_set || grow;
     if (requant) {
         float lo[3], hi[3];
         for (int k = 0; k < 3; ++k) {
@@ -287,8 +290,12 @@ arx_status ensure_device_scene(arx_renderer* r) {
                 lo[k] = std::min(lo[k], c->lo[k]);
                 hi[k] = std::max(hi[k], c->hi[k]);
             }
+            if (grow) {
+                lo[k] = std::min(lo[k], r->qgrid.origin[k]);
+                hi[k] = std::max(hi[k], r->qgrid.origin[k] + 65000.0f * r->qgrid.scale[k]);
+            }
         }
-        r->qgrid = make_qgrid(lo, hi);
+        r->qgrid = make_qgrid(lo, hi, grow ? 0.5 : 0.1);
         r->qgrid_set = true;
     }
     if (full || r->recv_dirty || requant) {

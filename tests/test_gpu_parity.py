@@ -195,8 +195,9 @@ def test_kernel_variants_identical(conference, monkeypatch, variant):
 @pytest.mark.parametrize("variant", ["900", "901", "921", "932", "940"])
 def test_quantized_nodes_regrid_and_fallback(c1_scene, monkeypatch, variant):
     """16-bit quantized nodes (QNode2): the grid covers scene + receiver + emitter at scene load.
-    A listener moved off the grid (outside the room) or an emitter off it makes the launches take
-    the f32 coded nodes until it is back on the grid; every case stays bit-exact with the oracle."""
+    A listener moved off the grid (outside the room) re-grids once (a wider grid, full
+    re-quantization); an emitter off the grid makes the launches take the f32 coded nodes.
+    Every case stays bit-exact with the oracle."""
     monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
     s = RenderSettings(rays=(64, 64, 4), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
     em = (0.5, 3.0, 1.0)
