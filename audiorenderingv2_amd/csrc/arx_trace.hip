@@ -1534,6 +1534,8 @@ template <int BLOCK, int STACK, int NF>
 __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
                                            int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs,
                                            int obase = 0) {
+    constexpr int FMT = NF & 15;  // NF >> 4: cache-policy bits of the QNode2 loads (design experiments)
+    constexpr int CP = NF >> 4;
     // the pop candidate is read first, so its LDS latency hides under the node fetch (the
     // slot sp - 1 is not touched by this step's write to slot sp)
     const int sp = t.sp;
@@ -1542,7 +1544,7 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
     float tn0, tf0, tn1, tf1;
     int c0, c1;
-    if constexpr (NF == 2) {
+    if constexpr (FMT == 2) {
         const int off = obase + t.node * (int)sizeof(QNode2);
         const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
@@ -1561,10 +1563,10 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
         c1 = (int)B.w;
     } else {
     float4 na, nb, nc;
-    if constexpr (NF == 1) {  // QNode2 (node_step7 Q16)
+    if constexpr (FMT == 1) {  // QNode2 (node_step7 Q16)
         const int off = t.node * (int)sizeof(QNode2);
-        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, CP));
+        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, CP));
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
         nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
         nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
@@ -1681,7 +1683,8 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 // waves whose rays ran long do not hold the launch open while others idle.
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
-    constexpr bool Q16 = NF >= 1;
+    constexpr int FMT = NF & 15;
+    constexpr bool Q16 = FMT >= 1;
     // STACK rows: sp <= bvh_depth < STACK (launch_v5), so the unconditional write to slot sp
     // stays in the array
     __shared__ int stk[STACK * BLOCK];
@@ -1756,7 +1759,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
                 r.inv[0] *= a.qgrid.scale[0];
                 r.inv[1] *= a.qgrid.scale[1];
                 r.inv[2] *= a.qgrid.scale[2];
-                if constexpr (NF == 2) {
+                if constexpr (FMT == 2) {
                     const int oct = (r.inv[0] < 0.0f ? 1 : 0) | (r.inv[1] < 0.0f ? 2 : 0) | (r.inv[2] < 0.0f ? 4 : 0);
                     obase = oct * (int)a.qostride * (int)sizeof(QNode2);
                 }
@@ -1783,7 +1786,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             if ((m_node | m_leaf) == 0ull) break;
             if (__popcll(__ballot(active && !trav)) >= THRESH) break;
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
-                if constexpr (NF == 3) {  // whole-wave steps (pair-cooperative fetch)
+                if constexpr (FMT == 3) {  // whole-wave steps (pair-cooperative fetch)
                     const int half = (lane & 1) * (int)sizeof(QChild);
 #pragma unroll
                     for (int k = 0; k < NSTEPS; ++k) {
@@ -2532,6 +2535,11 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 962: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 25>(a, cus, s);
         case 963: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 50>(a, cus, s);
         case 964: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 100>(a, cus, s);
+        // cache-policy bits on the node loads (aux = NF >> 4)
+        case 980: return launch_v5<128, 28, 12, 12, 5, 12, 17>(a, cus, s);
+        case 981: return launch_v5<128, 28, 12, 12, 5, 12, 33>(a, cus, s);
+        case 982: return launch_v5<128, 28, 12, 12, 5, 12, 49>(a, cus, s);
+        case 983: return launch_v5<128, 28, 12, 12, 5, 12, 65>(a, cus, s);
         // tunings of the default (921)
         case 950: return launch_v5<128, 28, 8, 12, 5, 12, 1>(a, cus, s);
         case 951: return launch_v5<128, 28, 16, 12, 5, 12, 1>(a, cus, s);
