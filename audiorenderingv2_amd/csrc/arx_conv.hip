@@ -26,6 +26,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -141,6 +142,71 @@ __device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, co
     }
 }
 
+// ---- 512-point FFTs (the 48 kHz plans): one wave per row / column, radix-8 in registers ----
+// Stockham radix-8 over 3 stages: each lane holds 8 elements (j + 64 r), so the row is loaded
+// and stored coalesced, the first stage starts from registers, the last one ends in them
+// (natural order), and only 2 LDS exchanges per FFT remain -- versus 5 stages x 2 block
+// barriers with half the threads idle in the generic radix-4 path.  A wave's LDS operations
+// execute in order, so the exchanges inside one wave need no block barrier.
+__device__ __forceinline__ double2 mul_w8(double2 a, int sign) {  // * e^(sign i pi/4)
+    const double c = 0.70710678118654752440;
+    return sign < 0 ? make_double2(c * (a.x + a.y), c * (a.y - a.x)) : make_double2(c * (a.x - a.y), c * (a.x + a.y));
+}
+__device__ __forceinline__ double2 mul_w83(double2 a, int sign) {  // * e^(sign 3 i pi/4)
+    const double c = 0.70710678118654752440;
+    return sign < 0 ? make_double2(c * (a.y - a.x), -c * (a.x + a.y)) : make_double2(-c * (a.x + a.y), c * (a.x - a.y));
+}
+// in-place 8-point DFT, y[q] = sum_r x[r] e^(sign 2 pi i r q / 8)
+__device__ __forceinline__ void dft8(double2* x, int sign) {
+    double2 a[4], b[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        a[r] = cadd(x[r], x[r + 4]);
+        b[r] = csub(x[r], x[r + 4]);
+    }
+    b[1] = mul_w8(b[1], sign);
+    b[2] = mul_si(b[2], sign);
+    b[3] = mul_w83(b[3], sign);
+    // 4-point DFTs of a (even outputs) and b (odd outputs)
+    const double2 a0 = cadd(a[0], a[2]), a1 = csub(a[0], a[2]), a2 = cadd(a[1], a[3]), a3 = mul_si(csub(a[1], a[3]), sign);
+    const double2 b0 = cadd(b[0], b[2]), b1 = csub(b[0], b[2]), b2 = cadd(b[1], b[3]), b3 = mul_si(csub(b[1], b[3]), sign);
+    x[0] = cadd(a0, a2);
+    x[4] = csub(a0, a2);
+    x[2] = cadd(a1, a3);
+    x[6] = csub(a1, a3);
+    x[1] = cadd(b0, b2);
+    x[5] = csub(b0, b2);
+    x[3] = cadd(b1, b3);
+    x[7] = csub(b1, b3);
+}
+// 512-point FFT of the row held as x[r] = element j + 64 r (lane j of the wave); result in the
+// same layout.  buf: the wave's 512-element LDS scratch; twl: W_512^e in LDS.
+__device__ __forceinline__ void fft512_wave(double2* x, double2* buf, const double2* twl, int j, int sign) {
+    dft8(x, sign);  // stage 1 (Ns = 1): no twiddles
+#pragma unroll
+    for (int q = 0; q < 8; ++q) buf[8 * j + q] = x[q];
+    __builtin_amdgcn_wave_barrier();
+    {  // stage 2 (Ns = 8)
+        const int k = j & 7;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = buf[j + 64 * r];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) x[r] = cmul(x[r], twiddle(twl, 512, 8 * r * k, sign));
+        dft8(x, sign);
+        const int d = (j - k) * 8 + k;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) buf[d + 8 * q] = x[q];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = buf[j + 64 * r];  // stage 3 (Ns = 64): k = j
+#pragma unroll
+    for (int r = 1; r < 8; ++r) x[r] = cmul(x[r], twiddle(twl, 512, r * j, sign));
+    dft8(x, sign);
+    __builtin_amdgcn_wave_barrier();
+}
+
 struct PassArgs {
     const double2* tw;
     int32_t M, N1, N2, lg1, lg2, tc;
@@ -198,7 +264,21 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
         lds[(size_t)c * a.N1 + n1] = x;
     }
     __syncthreads();
-    lds_fft(buf, a.N1, a.lg1, -1, t, per, twl, a.N1);
+    if (a.N1 == 512 && tc == 8) {  // 4 waves x 2 columns, radix-8 in registers (fft512_wave)
+        const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+        for (int cc = 0; cc < 2; ++cc) {
+            double2* cl = lds + (size_t)(2 * w + cc) * 512;
+            double2 x[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[r] = cl[j + 64 * r];
+            fft512_wave(x, cl, twl, j, -1);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) cl[j + 64 * r] = x[r];
+        }
+        __syncthreads();
+    } else {
+        lds_fft(buf, a.N1, a.lg1, -1, t, per, twl, a.N1);
+    }
     // twiddle W_M^(n2*k1) and store transposed: S[k1*N2 + n2]
     double2* dst = (MODE != 1) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
     for (int i = threadIdx.x; i < tc * a.N1; i += kThreads) {
@@ -252,6 +332,44 @@ __global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
     }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void pass_b512(PassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    constexpr int kRows = kThreads / 64;
+    const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+    const int k1 = blockIdx.x * kRows + w;
+    const int64_t batch = blockIdx.y;
+    double2* buf = lds + w * 512;
+    double2* twl = lds + kRows * 512;
+    for (int i = threadIdx.x; i < 512; i += kThreads) twl[i] = a.tw[(size_t)i * (a.M / 512)];
+    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * 512 : a.H + (size_t)batch * a.M + (int64_t)k1 * 512;
+    double2 x[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] = row[j + 64 * r];
+    __syncthreads();  // twiddle table
+    fft512_wave(x, buf, twl, j, -1);
+    if (MODE == 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) row[j + 64 * r] = x[r];
+        return;
+    }
+    double2 keep[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) keep[r] = x[r];
+    for (int c = 0; c < 2; ++c) {
+        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * 512;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x[r] = cmul(keep[r], Hc[j + 64 * r]);
+        fft512_wave(x, buf, twl, j, +1);
+        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * 512;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int i = j + 64 * r;
+            dst[i] = cmul(x[r], twiddle(a.tw, a.M, (int64_t)i * k1, +1));
+        }
+    }
+}
+
 // Pass C: inverse column FFTs of each (pair, channel) -> M * linear convolution of the
 // two blocks of the pair (re / im), written to Y for indices < n + sr - 1.
 __global__ __launch_bounds__(kThreads) void pass_c(PassArgs a) {
@@ -271,7 +389,21 @@ __global__ __launch_bounds__(kThreads) void pass_c(PassArgs a) {
         lds[(size_t)c * a.N1 + k1] = src[(int64_t)k1 * a.N2 + n2_0 + c];
     }
     __syncthreads();
-    lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, twl, a.N1);
+    if (a.N1 == 512 && tc == 8) {  // as in pass A
+        const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+        for (int cc = 0; cc < 2; ++cc) {
+            double2* cl = lds + (size_t)(2 * w + cc) * 512;
+            double2 x[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) x[r] = cl[j + 64 * r];
+            fft512_wave(x, cl, twl, j, +1);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) cl[j + 64 * r] = x[r];
+        }
+        __syncthreads();
+    } else {
+        lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, twl, a.N1);
+    }
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
     double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
     double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
@@ -377,6 +509,16 @@ void conv_plan_destroy(ConvPlan* p) {
 
 const char* conv_plan_describe(const ConvPlan* p) { return p ? p->desc : ""; }
 
+// The wave-per-row radix-8 pass B (pass_b512) for rows of 512; ARX_CONV_B512=0 takes the
+// generic radix-4 pass (design A/B).
+static bool use_b512(const ConvPlan* p) {
+    static const bool on = [] {
+        const char* e = std::getenv("ARX_CONV_B512");
+        return !(e && e[0] == '0');
+    }();
+    return on && p->N2 == 512 && p->N1 % 4 == 0;
+}
+
 static PassArgs base_args(const ConvPlan* p) {
     PassArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -400,8 +542,12 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
+    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
-    hipLaunchKernelGGL(pass_b<1>, dim3(p->N1, 2), dim3(kThreads), lds_b, s, a);
+    if (use_b512(p))
+        hipLaunchKernelGGL(pass_b512<1>, dim3(p->N1 / 4, 2), dim3(kThreads), lds_b512, s, a);
+    else
+        hipLaunchKernelGGL(pass_b<1>, dim3(p->N1, 2), dim3(kThreads), lds_b, s, a);
     return hipGetLastError();
 }
 
@@ -440,8 +586,12 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
+    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
-    hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
+    if (use_b512(p))
+        hipLaunchKernelGGL(pass_b512<0>, dim3(p->N1 / 4, (unsigned)pairs), dim3(kThreads), lds_b512, s, a);
+    else
+        hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
     return hipGetLastError();
@@ -474,8 +624,12 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
+    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
-    hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, 1), dim3(kThreads), lds_b, s, a);
+    if (use_b512(p))
+        hipLaunchKernelGGL(pass_b512<0>, dim3(p->N1 / 4, 1), dim3(kThreads), lds_b512, s, a);
+    else
+        hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, 1), dim3(kThreads), lds_b, s, a);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_d_live, dim3((unsigned)((p->n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
