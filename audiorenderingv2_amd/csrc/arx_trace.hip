@@ -1681,7 +1681,11 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 // POOL > 0: the last POOL percent of the rays form a shared pool that waves done with their
 // static range take from in refill-sized pieces (one atomic per refill, only near the end), so
 // waves whose rays ran long do not hold the launch open while others idle.
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
+// TAIL > 0: once the wave's rays are all handed out, the shading threshold drops from THRESH to
+// (live rays) / TAIL (at least 1), so finished queries of the last rays are shaded and
+// re-issued promptly instead of waiting for THRESH idle lanes that will never come.
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
+          int TAIL = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     constexpr int FMT = NF & 15;
     constexpr bool Q16 = FMT >= 1;
@@ -1784,7 +1788,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             const unsigned long long m_node = __ballot(t.node >= 0);
             const unsigned long long m_leaf = __ballot(t.node <= -2);
             if ((m_node | m_leaf) == 0ull) break;
-            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            int thr = THRESH;
+            if constexpr (TAIL > 0) {
+                if (exhausted) thr = min(THRESH, max(1, (int)__popcll(__ballot(active)) / TAIL));
+            }
+            if (__popcll(__ballot(active && !trav)) >= thr) break;
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
                 if constexpr (FMT == 3) {  // whole-wave steps (pair-cooperative fetch)
                     const int half = (lane & 1) * (int)sizeof(QChild);
@@ -2258,10 +2266,11 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
 }
 // v5 launcher: direction pre-pass + static per-wave ranges; trees deeper than the LDS stack
 // take the spill-stack v3 kernel, quantized variants without a usable grid the f32 nodes.
-template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0>
+template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
+          int TAIL = 0>
 hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
     if constexpr (NF >= 1) {
-        if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV, POOL>(args, cus, s);
+        if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV, POOL, TAIL>(args, cus, s);
     }
     if (args.bvh_depth + 1 > STACK) return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(args, cus, s);
     TraceArgs a = args;
@@ -2278,7 +2287,7 @@ hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
         const hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // pool cursor
         if (e != hipSuccess) return e;
     }
-    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL>;
+    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL>;
     const int grid = persistent_grid(k, BLOCK, n_rays, cus);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
@@ -2535,6 +2544,12 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 962: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 25>(a, cus, s);
         case 963: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 50>(a, cus, s);
         case 964: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 100>(a, cus, s);
+        // tail shading threshold (TAIL)
+        case 990: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 1>(a, cus, s);
+        case 991: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 2>(a, cus, s);
+        case 992: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 4>(a, cus, s);
+        case 993: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 8>(a, cus, s);
+        case 994: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 64>(a, cus, s);
         // cache-policy bits on the node loads (aux = NF >> 4)
         case 980: return launch_v5<128, 28, 12, 12, 5, 12, 17>(a, cus, s);
         case 981: return launch_v5<128, 28, 12, 12, 5, 12, 33>(a, cus, s);
