@@ -1051,4 +1051,29 @@ void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out) {
     }
 }
 
+bool quantize_wide16(const WideNode<4>* in, size_t n, const QGrid& g, QWide4* out) {
+    for (size_t i = 0; i < n; ++i) {
+        const WideNode<4>& w = in[i];
+        for (int c = 0; c < 4; ++c) {
+            const float lo[3] = {w.lox[c], w.loy[c], w.loz[c]};
+            const float hi[3] = {w.hix[c], w.hiy[c], w.hiz[c]};
+            const int32_t ref = w.ref[c], cnt = w.cnt[c];
+            const bool empty = cnt < 0;
+            for (int k = 0; k < 3; ++k) {
+                uint32_t ql = 1, qh = 0;  // empty: the slab between planes 0 and 1
+                if (!empty) {
+                    if (!(lo[k] <= hi[k])) return false;
+                    const int64_t l = q_lo(g, k, lo[k]), h = q_hi(g, k, hi[k]);
+                    if (l < 0 || h > 65535) return false;
+                    ql = (uint32_t)l;
+                    qh = (uint32_t)h;
+                }
+                out[i].c[c].q[k] = ql | (qh << 16);
+            }
+            out[i].c[c].code = empty ? kEmptyChildCode : cnt == 0 ? ref : ~(ref * 16 + cnt);
+        }
+    }
+    return true;
+}
+
 }  // namespace arx

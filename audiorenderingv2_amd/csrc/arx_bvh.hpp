@@ -80,6 +80,9 @@ bool quantize_nodes16(const BvhNode* coded, size_t n, const QGrid& g, QNode2* ou
 // negative component k): every axis word is (near | far << 16), i.e. lo and hi swapped on the
 // negative axes, so the slab test needs no min/max.  Octant 0 is the plain layout.
 void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out);
+// Quantized coded copy of WideNode<4> nodes on the grid (as quantize_nodes16); false if a box
+// leaves the grid.
+bool quantize_wide16(const WideNode<4>* in, size_t n, const QGrid& g, QWide4* out);
 
 // Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
 struct WideBuild {

@@ -93,6 +93,9 @@ struct arx_renderer {
     int wide_w = 0;
     WideBuild scene_w, recv_w;
     uint8_t* d_wnodes = nullptr;
+    QWide4* d_qwnodes = nullptr;  // quantized copy of d_wnodes (4-wide variants 1000+)
+    bool qw_valid = false;
+    uint32_t qgrid_gen = 0, qw_gen = ~0u;  // grid version / the version d_qwnodes was made on
     size_t wnodes_cap = 0;  // bytes
     int32_t* d_spill = nullptr;
     size_t spill_cap = 0;   // int32 entries
@@ -192,13 +195,17 @@ arx_status ensure_wide(arx_renderer* r, bool scene_changed, bool recv_changed) {
     const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
     if (total * nb > r->wnodes_cap) {
         if (r->d_wnodes) ARX_HIP(hipFree(r->d_wnodes));
+        if (r->d_qwnodes) ARX_HIP(hipFree(r->d_qwnodes));
         r->d_wnodes = nullptr;
+        r->d_qwnodes = nullptr;
         const size_t cap = (total + 256) * nb;
         ARX_HIP(hipMalloc(&r->d_wnodes, cap));
+        if (W == 4) ARX_HIP(hipMalloc(&r->d_qwnodes, (total + 256) * sizeof(QWide4)));
         r->wnodes_cap = cap;
         scene_new = true;
     }
-    if (!(scene_new || recv_new)) return ARX_OK;
+    const bool regrid = W == 4 && r->qw_gen != r->qgrid_gen;
+    if (!(scene_new || recv_new || regrid)) return ARX_OK;
     const char* why = "";
     if (scene_new && !validate_wide(W, r->scene_w.bytes.data(), 1, r->scene_w.count, total, n_tris, &why))
         return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (scene): %s", why);
@@ -215,6 +222,19 @@ arx_status ensure_wide(arx_renderer* r, bool scene_changed, bool recv_changed) {
     if (r->recv_w.count)
         ARX_HIP(hipMemcpyAsync(r->d_wnodes + (1 + r->scene_w.count) * nb, r->recv_w.bytes.data(),
                                r->recv_w.bytes.size(), hipMemcpyHostToDevice, r->stream));
+    if (W == 4 && r->d_qwnodes && r->qgrid_set) {
+        // quantized copy of the whole wide image (scene + top + receiver) on the current grid
+        std::vector<WideNode<4>> img(total);
+        std::memcpy(&img[0], top.data(), nb);
+        if (r->scene_w.count) std::memcpy(&img[1], r->scene_w.bytes.data(), r->scene_w.bytes.size());
+        if (r->recv_w.count) std::memcpy(&img[1 + r->scene_w.count], r->recv_w.bytes.data(), r->recv_w.bytes.size());
+        std::vector<QWide4> q(total);
+        r->qw_valid = quantize_wide16(img.data(), total, r->qgrid, q.data());
+        r->qw_gen = r->qgrid_gen;
+        if (r->qw_valid)
+            ARX_HIP(hipMemcpyAsync(r->d_qwnodes, q.data(), total * sizeof(QWide4), hipMemcpyHostToDevice, r->stream));
+        ARX_HIP(hipStreamSynchronize(r->stream));  // q is pageable and local
+    }
     // worst-case stack: every level of the deepest path leaves W-1 siblings behind
     const int depth = 1 + std::max(r->scene_w.depth, r->recv_w.depth);
     const int fanout = (W == kWideQ4) ? 4 : W;
@@ -297,6 +317,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
         }
         r->qgrid = make_qgrid(lo, hi, grow ? 0.5 : 0.1);
         r->qgrid_set = true;
+        ++r->qgrid_gen;
     }
     if (full || r->recv_dirty || requant) {
         BvhNode top = make_node(r->scene.root, r->recv.root);
@@ -505,6 +526,7 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_qnodes);
     hipFree(r->d_tris);
     hipFree(r->d_wnodes);
+    hipFree(r->d_qwnodes);
     hipFree(r->d_spill);
     hipFree(r->d_stash);
     hipFree(r->d_dirs);
@@ -667,6 +689,10 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.max_visits = (int32_t)std::min<size_t>(r->nodes_cap + 8, 0x7fffffff);
     a.bvh_depth = r->stats.bvh_depth;
     a.wnodes = r->d_wnodes;
+    {
+        const float* e = r->emitter;
+        a.qwnodes = (r->qw_valid && trace_width() == 4 && qgrid_contains(r->qgrid, e, e)) ? r->d_qwnodes : nullptr;
+    }
     a.spill = r->d_spill;
     a.spill_lanes = trace_spill_lanes(r->cus);
     a.stack_need = r->stack_need;

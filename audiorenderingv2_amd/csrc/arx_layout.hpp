@@ -83,6 +83,13 @@ struct alignas(16) QNode2 {
 };
 static_assert(sizeof(QNode2) == 32, "QNode2 must be 32 B");
 
+// 4-wide quantized node (variants 1000+): four QChild slots, child codes as in code_nodes (an
+// inner code is a wide-node index).
+struct alignas(16) QWide4 {
+    QChild c[4];
+};
+static_assert(sizeof(QWide4) == 64, "QWide4 must be 64 B");
+
 // The scene-wide grid of QNode2 trees.
 struct QGrid {
     float origin[3];
@@ -146,6 +153,8 @@ struct TraceArgs {
     QGrid qgrid;
     // octant copies (octant_nodes16): copy o of node i at qnodes[o * qostride + i], o = 0 plain
     uint32_t qostride;
+    // quantized copy of the 4-wide tree (wnodes, variants 1000+), same grid; null: unusable
+    const QWide4* qwnodes;
 };
 
 }  // namespace arx

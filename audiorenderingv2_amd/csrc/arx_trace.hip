@@ -1693,8 +1693,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     // stays in the array
     __shared__ int stk[STACK * BLOCK];
     const __amdgpu_buffer_rsrc_t nrs =
-        Q16 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
-            : node_rsrc(a.cnodes);
+        FMT == 5 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QWide4*>(a.qwnodes), (short)0, 0x7fffffff, 0x00020000)
+        : Q16    ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
+                 : node_rsrc(a.cnodes);
     const int lane = threadIdx.x;
     const uint64_t n = a.ray_end - a.ray_begin;
     const uint64_t n_static = POOL > 0 ? n - n * (uint64_t)POOL / 100 : n;  // [n_static, n): the pool
@@ -1705,7 +1706,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     bool pool = false;  // this wave has moved on to the shared pool
     unsigned long long* const cursor = a.counters + 4;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
-    const bool overflow = false;  // impossible by construction (node_step8)
+    bool overflow = false;  // impossible by construction for node_step8; NF 5 checks it
     bool active = false, trav = false, exhausted = POOL > 0 ? false : w_next >= w_end;
     RayState s;
     s.depth = -1;
@@ -1802,6 +1803,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
                         if (__ballot(go) == 0ull) break;
                         node_step8p<BLOCK, STACK>(r, oix, oiy, oiz, t, stk, lane, nrs, go, half);
                     }
+                } else if constexpr (FMT == 5) {
+#pragma unroll
+                    for (int k = 0; k < NSTEPS; ++k)
+                        if (t.node >= 0) node_step8w<BLOCK, STACK, NF>(r, oix, oiy, oiz, t, stk, lane, nrs, overflow);
                 } else {
 #pragma unroll
                     for (int k = 0; k < NSTEPS; ++k)
@@ -1853,6 +1858,62 @@ __device__ __forceinline__ void sort_children(float* k, int* v) {
         cswap(k[1], v[1], k[2], v[2]); cswap(k[3], v[3], k[4], v[4]);
         cswap(k[5], v[5], k[6], v[6]);
     }
+}
+
+// NF 5: branch-free step over 4-wide quantized nodes (QWide4, 64 B = four 16-B child records):
+// about half the dependent node fetches of the binary tree per query.  All four child slabs are
+// tested, the hit children sorted by entry distance (misses keyed +inf), the nearest becomes the
+// next entry and the other hits are written far to near above the top of the stack.  The three
+// slot writes are unconditional and issued from the highest slot down, so a write clamped to
+// row STACK - 1 is overwritten by the valid one.  The stack holds up to three entries per wide
+// level, more than STACK for the deepest trees: *ovf is set if a push would leave the array
+// (the host then reports the overflow).
+__device__ __forceinline__ void qchild_slab(uint4 c, float ix, float iy, float iz, float oix, float oiy, float oiz,
+                                            float best_t, float& key, int& code, int& hit) {
+    const float x0 = __builtin_fmaf((float)(c.x & 0xffffu), ix, -oix), x1 = __builtin_fmaf((float)(c.x >> 16), ix, -oix);
+    const float y0 = __builtin_fmaf((float)(c.y & 0xffffu), iy, -oiy), y1 = __builtin_fmaf((float)(c.y >> 16), iy, -oiy);
+    const float z0 = __builtin_fmaf((float)(c.z & 0xffffu), iz, -oiz), z1 = __builtin_fmaf((float)(c.z >> 16), iz, -oiz);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), best_t));
+    const bool h = tn <= tf;
+    key = h ? tn : __builtin_huge_valf();
+    code = (int)c.w;
+    hit = (int)h;
+}
+
+template <int BLOCK, int STACK, int NF>
+__device__ __forceinline__ void node_step8w(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                            int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs, bool& ovf) {
+    constexpr int CP = NF >> 4;
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
+    const int off = t.node * (int)sizeof(QWide4);
+    const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, CP));
+    const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, CP));
+    const uint4 C = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32, 0, CP));
+    const uint4 D = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 48, 0, CP));
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    float k[4];
+    int v[4], h[4];
+    qchild_slab(A, ix, iy, iz, oix, oiy, oiz, t.best_t, k[0], v[0], h[0]);
+    qchild_slab(B, ix, iy, iz, oix, oiy, oiz, t.best_t, k[1], v[1], h[1]);
+    qchild_slab(C, ix, iy, iz, oix, oiy, oiz, t.best_t, k[2], v[2], h[2]);
+    qchild_slab(D, ix, iy, iz, oix, oiy, oiz, t.best_t, k[3], v[3], h[3]);
+    const int nh = h[0] + h[1] + h[2] + h[3];
+    sort_children<4>(k, v);
+    const int s0 = nh == 4 ? v[3] : (nh == 3 ? v[2] : v[1]);
+    const int s1 = nh == 4 ? v[2] : v[1];
+    stk[min(sp + 2, STACK - 1) * BLOCK + lane] = v[1];
+    stk[min(sp + 1, STACK - 1) * BLOCK + lane] = s1;
+    stk[min(sp, STACK - 1) * BLOCK + lane] = s0;
+    asm volatile("" : "+v"(top));
+    const bool any = nh > 0;
+    const int popped = sp > 0 ? top : -1;
+    const int ns = sp + nh - 1;
+    ovf = ovf | (ns > STACK);
+    t.node = any ? v[0] : popped;
+    t.sp = any ? ns : sp_pop;
 }
 
 template <int W, int BLOCK, int S>
@@ -2269,10 +2330,12 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
           int TAIL = 0>
 hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
-    if constexpr (NF >= 1) {
+    if constexpr ((NF & 15) == 5) {  // 4-wide quantized: without its grid copy, the binary steps
+        if (!args.qwnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, 12, 1, LV, POOL, TAIL>(args, cus, s);
+    } else if constexpr (NF >= 1) {
         if (!args.qnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, 0, LV, POOL, TAIL>(args, cus, s);
     }
-    if (args.bvh_depth + 1 > STACK) return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(args, cus, s);
+    if ((NF & 15) != 5 && args.bvh_depth + 1 > STACK) return launch_v3<128, 12, 12, 28, 5, false, 1, 71, 3>(args, cus, s);
     TraceArgs a = args;
     a.static_ranges = 1;
     a.dirs = nullptr;
@@ -2299,6 +2362,7 @@ int trace_width() {
     if (v >= 300 && v < 310) return 4;
     if (v >= 310 && v < 320) return 8;
     if ((v >= 320 && v < 340) || (v >= 720 && v < 730)) return kWideQ4;
+    if (v >= 1000 && v < 1010) return 4;  // QWide4 copy of the 4-wide tree (trace_kernel_v5 NF 5)
     return 2;
 }
 
@@ -2555,6 +2619,16 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 981: return launch_v5<128, 28, 12, 12, 5, 12, 33>(a, cus, s);
         case 982: return launch_v5<128, 28, 12, 12, 5, 12, 49>(a, cus, s);
         case 983: return launch_v5<128, 28, 12, 12, 5, 12, 65>(a, cus, s);
+        // 4-wide quantized branch-free steps (node_step8w)
+        case 1000: return launch_v5<128, 28, 12, 12, 5, 8, 5>(a, cus, s);
+        case 1001: return launch_v5<128, 28, 12, 12, 4, 8, 5>(a, cus, s);
+        case 1002: return launch_v5<128, 28, 12, 12, 5, 6, 5>(a, cus, s);
+        case 1003: return launch_v5<128, 28, 12, 8, 5, 8, 5>(a, cus, s);
+        case 1004: return launch_v5<128, 28, 12, 12, 5, 4, 5>(a, cus, s);
+        case 1005: return launch_v5<128, 28, 12, 12, 5, 5, 5>(a, cus, s);
+        case 1006: return launch_v5<128, 28, 12, 16, 5, 6, 5>(a, cus, s);
+        case 1007: return launch_v5<128, 28, 16, 12, 5, 6, 5>(a, cus, s);
+        case 1008: return launch_v5<128, 28, 12, 12, 5, 3, 5>(a, cus, s);
         // tunings of the default (921)
         case 950: return launch_v5<128, 28, 8, 12, 5, 12, 1>(a, cus, s);
         case 951: return launch_v5<128, 28, 16, 12, 5, 12, 1>(a, cus, s);

@@ -155,7 +155,7 @@ def test_full_size_c3_properties(conference):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
 
 
-@pytest.mark.parametrize("variant", ["300", "307", "310", "312", "320", "323", "720", "900", "901", "920", "921", "932", "940"])
+@pytest.mark.parametrize("variant", ["300", "307", "310", "312", "320", "323", "720", "900", "901", "920", "921", "932", "940", "1000", "1002"])
 def test_wide_tree_variants_match_oracle(c1_scene, conference, monkeypatch, variant):
     """4- and 8-wide trees (incl. LDS-stack spill variants) against the oracle: C1 dense,
     a listener move (receiver-only re-collapse) and an empty scene."""
@@ -176,7 +176,7 @@ def test_wide_tree_variants_match_oracle(c1_scene, conference, monkeypatch, vari
     assert st["receiver_hits"] > 0
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312", "320", "322", "323", "400", "401", "500", "501", "505", "600", "601", "606", "701", "702", "703", "706", "720", "722", "730", "732", "800", "802", "804", "810", "812", "740", "742", "745", "751", "760", "763", "767", "770", "772", "780", "781", "792", "794", "863", "861", "900", "901", "903", "905", "907", "920", "921", "923", "927", "930", "931", "778", "932", "933", "940", "941"])
+@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312", "320", "322", "323", "400", "401", "500", "501", "505", "600", "601", "606", "701", "702", "703", "706", "720", "722", "730", "732", "800", "802", "804", "810", "812", "740", "742", "745", "751", "760", "763", "767", "770", "772", "780", "781", "792", "794", "863", "861", "900", "901", "903", "905", "907", "920", "921", "923", "927", "930", "931", "778", "932", "933", "940", "941", "1000", "1002", "1004"])
 def test_kernel_variants_identical(conference, monkeypatch, variant):
     """Every trace-kernel variant (grid-stride v1, persistent v2, postponed-leaf v3 and its
     tunings, 4-/8-wide trees) produces the default kernel's histogram bit for bit."""
@@ -192,7 +192,7 @@ def test_kernel_variants_identical(conference, monkeypatch, variant):
     assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
 
 
-@pytest.mark.parametrize("variant", ["900", "901", "921", "932", "940"])
+@pytest.mark.parametrize("variant", ["900", "901", "921", "932", "940", "1002"])
 def test_quantized_nodes_regrid_and_fallback(c1_scene, monkeypatch, variant):
     """16-bit quantized nodes (QNode2): the grid covers scene + receiver + emitter at scene load.
     A listener moved off the grid (outside the room) re-grids once (a wider grid, full
