@@ -653,6 +653,34 @@ void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset) {
     fix(b.root.ref, b.root.count);
 }
 
+void bfs_prefix_order(BvhBuild& b, size_t k) {
+    const size_t n = b.nodes.size();
+    if (n == 0 || b.root.count != 0) return;
+    k = std::min(k, n);
+    std::vector<int32_t> order;  // the first k inner nodes in breadth-first order
+    order.reserve(k);
+    order.push_back(b.root.ref);
+    for (size_t h = 0; h < order.size() && order.size() < k; ++h) {
+        const BvhNode& nd = b.nodes[(size_t)order[h]];
+        for (int c = 0; c < 2 && order.size() < k; ++c)
+            if (nd.d[2 + c] == 0) order.push_back(nd.d[c]);
+    }
+    std::vector<int32_t> map(n, -1);
+    int32_t next = 0;
+    for (int32_t i : order) map[(size_t)i] = next++;
+    for (size_t i = 0; i < n; ++i)  // the rest keep their relative order (parents before children)
+        if (map[i] < 0) map[i] = next++;
+    std::vector<BvhNode> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        BvhNode nd = b.nodes[i];
+        for (int c = 0; c < 2; ++c)
+            if (nd.d[2 + c] == 0) nd.d[c] = map[(size_t)nd.d[c]];
+        out[(size_t)map[i]] = nd;
+    }
+    b.nodes.swap(out);
+    b.root.ref = map[(size_t)b.root.ref];
+}
+
 namespace {
 
 ChildRef child_of(const BvhNode& n, int c) {

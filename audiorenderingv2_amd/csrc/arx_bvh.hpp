@@ -51,6 +51,10 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 // Shift all node / triangle references by the given offsets (placing the build inside a
 // bigger array).  The root reference is shifted too.
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
+// Renumber the nodes so the first k inner nodes in breadth-first order from the root take
+// indices 0..k-1 (the rest keep their order, so parents still precede their children): the
+// trace kernel keeps the top of the scene tree in LDS (trace_kernel_v5 LCACHE).
+void bfs_prefix_order(BvhBuild& b, size_t k);
 BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
 ChildRef empty_child();
 // Structural check of a device-ready node array (acyclic, references in range).

@@ -563,6 +563,7 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
     for (int64_t i = 0; i < 9 * n; ++i)
         if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
+    bfs_prefix_order(r->scene, 1023);  // the kernels' LDS node cache holds the top of the tree
     relocate_bvh(r->scene, 1, 0);
     r->n_scene = n;
     r->scene_set = true;
@@ -663,6 +664,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         a.qnodes = (r->q_valid && oct_ok && qgrid_contains(r->qgrid, e, e)) ? r->d_qnodes : nullptr;
         a.qgrid = r->qgrid;
         a.qostride = (uint32_t)r->nodes_cap;
+        a.qcount = (uint32_t)(1 + r->scene.nodes.size() + r->recv.nodes.size());
     }
     a.tris = r->d_tris;
     a.hist = r->hist();

@@ -155,6 +155,7 @@ struct TraceArgs {
     uint32_t qostride;
     // quantized copy of the 4-wide tree (wnodes, variants 1000+), same grid; null: unusable
     const QWide4* qwnodes;
+    uint32_t qcount;  // nodes in cnodes / qnodes (top + scene + receiver)
 };
 
 }  // namespace arx

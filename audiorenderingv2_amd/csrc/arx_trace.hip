@@ -1607,6 +1607,53 @@ __device__ __forceinline__ void node_step8(const Ray& r, float oix, float oiy, f
     t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
 }
 
+// NF 6: node_step8 over QNode2 with the top LC nodes (the top node and the scene tree's
+// breadth-first prefix, bfs_prefix_order) held in LDS: those lanes read the node from LDS, the
+// others from memory, so the vector-memory data path (TD, ~90 % busy) carries only the deeper
+// steps.  The two reads are exec-masked (one branch pair per step).
+template <int BLOCK, int STACK, int LC>
+__device__ __forceinline__ void node_step8c(const Ray& r, float oix, float oiy, float oiz, Trav3& t,
+                                            int* __restrict__ stk, int lane, __amdgpu_buffer_rsrc_t rs,
+                                            const uint4* __restrict__ lcache) {
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk[sp_pop * BLOCK + lane];
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    uint4 A, B;
+    if (t.node < LC) {
+        A = lcache[2 * t.node];
+        B = lcache[2 * t.node + 1];
+    } else {
+        const int off = t.node * (int)sizeof(QNode2);
+        A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+    }
+    const float4 na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
+    const float4 nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
+    const float4 nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
+    const int c0 = (int)A.w, c1 = (int)B.w;
+    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+    const bool near1 = h1 & (!h0 | (tn1 < tn0));
+    const int c_near = near1 ? c1 : c0;
+    const int c_far = near1 ? c0 : c1;
+    stk[min(sp, STACK - 1) * BLOCK + lane] = c_far;
+    asm volatile("" : "+v"(top));
+    const bool any = h0 | h1;
+    const int popped = sp > 0 ? top : -1;
+    t.node = any ? c_near : popped;
+    t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
+}
+
 // NF 3: pair-cooperative fetch of QNode2 nodes.  The vector-memory data path is charged per
 // distinct 64-B block per wave-instruction (td_microbench), and two per-lane 16-B loads of a
 // 32-B node touch 2 x 64 blocks per step.  Here lane pair (2p, 2p+1) fetches its two nodes
@@ -1685,13 +1732,14 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 // (live rays) / TAIL (at least 1), so finished queries of the last rays are shaded and
 // re-issued promptly instead of waiting for THRESH idle lanes that will never come.
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
-          int TAIL = 0>
+          int TAIL = 0, int LC = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     constexpr int FMT = NF & 15;
     constexpr bool Q16 = FMT >= 1;
     // STACK rows: sp <= bvh_depth < STACK (launch_v5), so the unconditional write to slot sp
     // stays in the array
-    __shared__ int stk[STACK * BLOCK];
+    // NF 6: LC cached nodes (8 ints each) after the stack rows
+    __shared__ int stk[STACK * BLOCK + (FMT == 6 ? 8 * LC : 0)];
     const __amdgpu_buffer_rsrc_t nrs =
         FMT == 5 ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QWide4*>(a.qwnodes), (short)0, 0x7fffffff, 0x00020000)
         : Q16    ? __builtin_amdgcn_make_buffer_rsrc(const_cast<QNode2*>(a.qnodes), (short)0, 0x7fffffff, 0x00020000)
@@ -1722,6 +1770,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     t.visits = 0;
     float oix = 0.f, oiy = 0.f, oiz = 0.f;
     int obase = 0;  // NF 2: byte offset of the ray's octant copy
+    uint4* const lcache = reinterpret_cast<uint4*>(stk + STACK * BLOCK);
+    if constexpr (FMT == 6) {  // the top LC nodes (a.qcount valid ones) into LDS
+        for (int i = lane; i < 2 * LC; i += BLOCK) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if ((uint32_t)(i >> 1) < a.qcount)
+                v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nrs, i * 16, 0, 0));
+            lcache[i] = v;
+        }
+        __syncthreads();
+    }
     while (true) {
         if (active && !trav) {
             shade(a, s, r, t.best, n_rx, n_miss);
@@ -1803,6 +1861,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
                         if (__ballot(go) == 0ull) break;
                         node_step8p<BLOCK, STACK>(r, oix, oiy, oiz, t, stk, lane, nrs, go, half);
                     }
+                } else if constexpr (FMT == 6) {
+#pragma unroll
+                    for (int k = 0; k < NSTEPS; ++k)
+                        if (t.node >= 0) node_step8c<BLOCK, STACK, LC>(r, oix, oiy, oiz, t, stk, lane, nrs, lcache);
                 } else if constexpr (FMT == 5) {
 #pragma unroll
                     for (int k = 0; k < NSTEPS; ++k)
@@ -2328,7 +2390,7 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
 // v5 launcher: direction pre-pass + static per-wave ranges; trees deeper than the LDS stack
 // take the spill-stack v3 kernel, quantized variants without a usable grid the f32 nodes.
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
-          int TAIL = 0>
+          int TAIL = 0, int LC = 0>
 hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
     if constexpr ((NF & 15) == 5) {  // 4-wide quantized: without its grid copy, the binary steps
         if (!args.qwnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, 12, 1, LV, POOL, TAIL>(args, cus, s);
@@ -2350,7 +2412,7 @@ hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
         const hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // pool cursor
         if (e != hipSuccess) return e;
     }
-    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL>;
+    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL, LC>;
     const int grid = persistent_grid(k, BLOCK, n_rays, cus);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
@@ -2362,7 +2424,7 @@ int trace_width() {
     if (v >= 300 && v < 310) return 4;
     if (v >= 310 && v < 320) return 8;
     if ((v >= 320 && v < 340) || (v >= 720 && v < 730)) return kWideQ4;
-    if (v >= 1000 && v < 1010) return 4;  // QWide4 copy of the 4-wide tree (trace_kernel_v5 NF 5)
+    if (v >= 1000 && v < 1020) return 4;  // QWide4 copy of the 4-wide tree (trace_kernel_v5 NF 5)
     return 2;
 }
 
@@ -2629,6 +2691,16 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 1006: return launch_v5<128, 28, 12, 16, 5, 6, 5>(a, cus, s);
         case 1007: return launch_v5<128, 28, 16, 12, 5, 6, 5>(a, cus, s);
         case 1008: return launch_v5<128, 28, 12, 12, 5, 3, 5>(a, cus, s);
+        case 1009: return launch_v5<128, 28, 12, 12, 5, 6, 5, 1, 0, 8>(a, cus, s);
+        case 1010: return launch_v5<128, 28, 12, 12, 5, 6, 5, 1, 0, 64>(a, cus, s);
+        // top of the tree in LDS (node_step8c): 64 / 32 nodes per 128-lane block, 128 per 256,
+        // 320 per 640 (10 waves, 2 blocks per CU)
+        case 1100: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 64>(a, cus, s);
+        case 1101: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 32>(a, cus, s);
+        case 1102: return launch_v5<256, 28, 12, 12, 5, 12, 6, 1, 0, 0, 128>(a, cus, s);
+        case 1103: return launch_v5<640, 28, 12, 12, 5, 12, 6, 1, 0, 0, 320>(a, cus, s);
+        case 1104: return launch_v5<256, 28, 12, 12, 5, 12, 1>(a, cus, s);
+        case 1105: return launch_v5<640, 28, 12, 12, 5, 12, 1>(a, cus, s);
         // tunings of the default (921)
         case 950: return launch_v5<128, 28, 8, 12, 5, 12, 1>(a, cus, s);
         case 951: return launch_v5<128, 28, 16, 12, 5, 12, 1>(a, cus, s);

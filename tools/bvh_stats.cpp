@@ -56,12 +56,23 @@ static bool slab(const float lo[3], const float hi[3], const Q& q, float tmax, f
 
 struct Stats {
     double visits = 0, tests = 0, leaves = 0, maxstack = 0;
+    double shallow[8] = {};  // visits to nodes at depth <= 2 + k below the top node
 };
 
 struct Tree {
     int W;
     std::vector<ChildRef> kids;  // W per node
     size_t n = 0;
+    std::vector<int> depth;  // node depth below the top node (0)
+    void set_depths() {
+        depth.assign(n, 1 << 20);
+        depth[0] = 0;
+        for (size_t i = 0; i < n; ++i)  // parents come before their children
+            for (int s = 0; s < W; ++s) {
+                const ChildRef& c = kids[(size_t)W * i + s];
+                if (c.count == 0 && c.ref >= 0 && (size_t)c.ref < n) depth[c.ref] = std::min(depth[c.ref], depth[i] + 1);
+            }
+    }
 };
 
 static Tree from_binary(const std::vector<BvhNode>& nodes, const BvhNode& top) {
@@ -155,6 +166,8 @@ static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Sta
             continue;
         }
         st.visits += 1;
+        if (!t.depth.empty())
+            for (int k = 0; k < 8; ++k) st.shallow[k] += t.depth[code] <= 2 + k ? 1 : 0;
         std::vector<std::pair<float, int>> hits;
         for (int s = 0; s < t.W; ++s) {
             const ChildRef& c = t.kids[(size_t)t.W * code + s];
@@ -214,6 +227,15 @@ int main(int argc, char** argv) {
     std::printf("spatial %d alpha %g budget %g: refs %zu\n", (int)bp.spatial, bp.spatial_alpha, bp.spatial_budget, b.tris.size());
     std::printf("tris %ld  binary nodes %zu depth %d | wide4 %zu depth %d | wide8 %zu depth %d\n", n, b.nodes.size(),
                 b.depth, w4.count, w4.depth, w8.count, w8.depth);
+    t2.set_depths();
+    {
+        long cnt[40] = {};
+        for (size_t i = 0; i < t2.n; ++i) if (t2.depth[i] < 40) ++cnt[t2.depth[i]];
+        long cum = 0;
+        std::printf("binary nodes by depth (cumulative):");
+        for (int d = 0; d < 12; ++d) std::printf(" %d:%ld", d, cum += cnt[d]);
+        std::printf("\n");
+    }
     Tree* trees[4] = {&t2, &t4, &t8, &tq};
     const double node_bytes[4] = {64, 128, 256, 64};
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
@@ -253,6 +275,11 @@ int main(int argc, char** argv) {
         std::printf("W=%d: %ld queries  visits %.1f  leaves %.1f  tri tests %.1f  node bytes %.0f  tri bytes %.0f  "
                     "max stack %.0f\n",
                     trees[k]->W, queries, v, lv, te, v * node_bytes[k], te * 48.0, st.maxstack);
+        if (k == 0) {
+            std::printf("   share of visits at depth <=");
+            for (int d = 0; d < 8; ++d) std::printf(" %d: %.3f", 2 + d, st.shallow[d] / st.visits);
+            std::printf("\n");
+        }
     }
     return 0;
 }

@@ -15,7 +15,9 @@ from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  
 def main():
     variants = [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "1,2,3,4,5,6,7".split(","))]
     sr = int(os.environ.get("SR", "48000"))
-    s = RenderSettings(rays=(100, 100, 100), sample_rate=sr, base_power=3.62, max_bounces=16)
+    rays = tuple(int(x) for x in os.environ.get("RAYS", "100,100,100").split(","))
+    bounces = int(os.environ.get("BOUNCES", "16"))
+    s = RenderSettings(rays=rays, sample_rate=sr, base_power=3.62, max_bounces=bounces)
     r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
     r.setEmitterPosInOptix(CONFERENCE_EMITTER)
     r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
