@@ -207,6 +207,72 @@ __device__ __forceinline__ void fft512_wave(double2* x, double2* buf, const doub
     __builtin_amdgcn_wave_barrier();
 }
 
+// ---- 256-point FFTs (the 16 kHz plans, M = 2^16 = 256 x 256): one wave per row / column,
+// four radix-4 Stockham stages, each lane one butterfly per stage on elements j + 64 r (the
+// lane's registers), so the first stage starts from registers, the last one ends in them in
+// natural order, and 3 in-wave LDS exchanges remain.
+__device__ __forceinline__ void dft4(double2* x, int sign) {
+    const double2 a0 = cadd(x[0], x[2]), a1 = csub(x[0], x[2]), a2 = cadd(x[1], x[3]), a3 = mul_si(csub(x[1], x[3]), sign);
+    x[0] = cadd(a0, a2);
+    x[1] = cadd(a1, a3);
+    x[2] = csub(a0, a2);
+    x[3] = csub(a1, a3);
+}
+__device__ __forceinline__ void fft256_wave(double2* x, double2* buf, const double2* twl, int j, int sign) {
+    dft4(x, sign);  // Ns = 1: no twiddles
+#pragma unroll
+    for (int q = 0; q < 4; ++q) buf[4 * j + q] = x[q];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int Ns = 4; Ns <= 16; Ns *= 4) {
+        const int k = j & (Ns - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = buf[j + 64 * r];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) x[r] = cmul(x[r], twiddle(twl, 256, (64 / Ns) * r * k, sign));
+        dft4(x, sign);
+        const int d = (j - k) * 4 + k;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) buf[d + Ns * q] = x[q];
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = buf[j + 64 * r];  // Ns = 64: k = j
+#pragma unroll
+    for (int r = 1; r < 4; ++r) x[r] = cmul(x[r], twiddle(twl, 256, r * j, sign));
+    dft4(x, sign);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// L-point wave FFT of x[r] = element j + 64 r (L = 256 or 512)
+template <int L>
+__device__ __forceinline__ void fft_wave(double2* x, double2* buf, const double2* twl, int j, int sign) {
+    if constexpr (L == 512)
+        fft512_wave(x, buf, twl, j, sign);
+    else
+        fft256_wave(x, buf, twl, j, sign);
+}
+
+// Column FFTs of the tile in LDS (tc columns of L, then the twiddle table) by the block's
+// 4 waves, tc / 4 columns each.
+template <int L>
+__device__ __forceinline__ void columns_wave(double2* lds, const double2* twl, int tc, int sign) {
+    constexpr int R = L / 64;
+    const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+    const int per_wave = tc / 4;
+    for (int cc = 0; cc < per_wave; ++cc) {
+        double2* cl = lds + (size_t)(per_wave * w + cc) * L;
+        double2 x[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = cl[j + 64 * r];
+        fft_wave<L>(x, cl, twl, j, sign);
+#pragma unroll
+        for (int r = 0; r < R; ++r) cl[j + 64 * r] = x[r];
+    }
+    __syncthreads();
+}
+
 struct PassArgs {
     const double2* tw;
     int32_t M, N1, N2, lg1, lg2, tc;
@@ -265,17 +331,9 @@ __global__ __launch_bounds__(kThreads) void pass_a(PassArgs a) {
     }
     __syncthreads();
     if (a.N1 == 512 && tc == 8) {  // 4 waves x 2 columns, radix-8 in registers (fft512_wave)
-        const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
-        for (int cc = 0; cc < 2; ++cc) {
-            double2* cl = lds + (size_t)(2 * w + cc) * 512;
-            double2 x[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) x[r] = cl[j + 64 * r];
-            fft512_wave(x, cl, twl, j, -1);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) cl[j + 64 * r] = x[r];
-        }
-        __syncthreads();
+        columns_wave<512>(lds, twl, tc, -1);
+    } else if (a.N1 == 256 && tc == 16) {  // 4 waves x 4 columns, radix-4 in registers
+        columns_wave<256>(lds, twl, tc, -1);
     } else {
         lds_fft(buf, a.N1, a.lg1, -1, t, per, twl, a.N1);
     }
@@ -332,38 +390,39 @@ __global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kThreads) void pass_b512(PassArgs a) {
+template <int MODE, int L>
+__global__ __launch_bounds__(kThreads) void pass_bw(PassArgs a) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     constexpr int kRows = kThreads / 64;
+    constexpr int R = L / 64;
     const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
     const int k1 = blockIdx.x * kRows + w;
     const int64_t batch = blockIdx.y;
-    double2* buf = lds + w * 512;
-    double2* twl = lds + kRows * 512;
-    for (int i = threadIdx.x; i < 512; i += kThreads) twl[i] = a.tw[(size_t)i * (a.M / 512)];
-    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * 512 : a.H + (size_t)batch * a.M + (int64_t)k1 * 512;
-    double2 x[8];
+    double2* buf = lds + w * L;
+    double2* twl = lds + kRows * L;
+    for (int i = threadIdx.x; i < L; i += kThreads) twl[i] = a.tw[(size_t)i * (a.M / L)];
+    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * L : a.H + (size_t)batch * a.M + (int64_t)k1 * L;
+    double2 x[R];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] = row[j + 64 * r];
+    for (int r = 0; r < R; ++r) x[r] = row[j + 64 * r];
     __syncthreads();  // twiddle table
-    fft512_wave(x, buf, twl, j, -1);
+    fft_wave<L>(x, buf, twl, j, -1);
     if (MODE == 1) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) row[j + 64 * r] = x[r];
+        for (int r = 0; r < R; ++r) row[j + 64 * r] = x[r];
         return;
     }
-    double2 keep[8];
+    double2 keep[R];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) keep[r] = x[r];
+    for (int r = 0; r < R; ++r) keep[r] = x[r];
     for (int c = 0; c < 2; ++c) {
-        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * 512;
+        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * L;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) x[r] = cmul(keep[r], Hc[j + 64 * r]);
-        fft512_wave(x, buf, twl, j, +1);
-        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * 512;
+        for (int r = 0; r < R; ++r) x[r] = cmul(keep[r], Hc[j + 64 * r]);
+        fft_wave<L>(x, buf, twl, j, +1);
+        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * L;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < R; ++r) {
             const int i = j + 64 * r;
             dst[i] = cmul(x[r], twiddle(a.tw, a.M, (int64_t)i * k1, +1));
         }
@@ -390,17 +449,9 @@ __global__ __launch_bounds__(kThreads) void pass_c(PassArgs a) {
     }
     __syncthreads();
     if (a.N1 == 512 && tc == 8) {  // as in pass A
-        const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
-        for (int cc = 0; cc < 2; ++cc) {
-            double2* cl = lds + (size_t)(2 * w + cc) * 512;
-            double2 x[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) x[r] = cl[j + 64 * r];
-            fft512_wave(x, cl, twl, j, +1);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) cl[j + 64 * r] = x[r];
-        }
-        __syncthreads();
+        columns_wave<512>(lds, twl, tc, +1);
+    } else if (a.N1 == 256 && tc == 16) {
+        columns_wave<256>(lds, twl, tc, +1);
     } else {
         lds_fft(lds + (size_t)col * a.N1, a.N1, a.lg1, +1, t, per, twl, a.N1);
     }
@@ -509,14 +560,20 @@ void conv_plan_destroy(ConvPlan* p) {
 
 const char* conv_plan_describe(const ConvPlan* p) { return p ? p->desc : ""; }
 
-// The wave-per-row radix-8 pass B (pass_b512) for rows of 512; ARX_CONV_B512=0 takes the
+// Pass B: the wave-per-row pass (pass_bw) for rows of 512 or 256; ARX_CONV_B512=0 takes the
 // generic radix-4 pass (design A/B).
-static bool use_b512(const ConvPlan* p) {
+template <int MODE>
+static void launch_pass_b(const ConvPlan* p, unsigned batches, const PassArgs& a, hipStream_t s) {
     static const bool on = [] {
         const char* e = std::getenv("ARX_CONV_B512");
         return !(e && e[0] == '0');
     }();
-    return on && p->N2 == 512 && p->N1 % 4 == 0;
+    if (on && p->N2 == 512 && p->N1 % 4 == 0)
+        hipLaunchKernelGGL((pass_bw<MODE, 512>), dim3(p->N1 / 4, batches), dim3(kThreads), (4 + 1) * 512 * sizeof(double2), s, a);
+    else if (on && p->N2 == 256 && p->N1 % 4 == 0)
+        hipLaunchKernelGGL((pass_bw<MODE, 256>), dim3(p->N1 / 4, batches), dim3(kThreads), (4 + 1) * 256 * sizeof(double2), s, a);
+    else
+        hipLaunchKernelGGL(pass_b<MODE>, dim3(p->N1, batches), dim3(kThreads), 2 * (size_t)p->N2 * sizeof(double2), s, a);
 }
 
 static PassArgs base_args(const ConvPlan* p) {
@@ -541,13 +598,8 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     a.ir_l = d_ir_left;
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
-    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
-    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
-    if (use_b512(p))
-        hipLaunchKernelGGL(pass_b512<1>, dim3(p->N1 / 4, 2), dim3(kThreads), lds_b512, s, a);
-    else
-        hipLaunchKernelGGL(pass_b<1>, dim3(p->N1, 2), dim3(kThreads), lds_b, s, a);
+    launch_pass_b<1>(p, 2, a, s);
     return hipGetLastError();
 }
 
@@ -585,13 +637,8 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.out_r = d_out_right;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
-    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
-    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
-    if (use_b512(p))
-        hipLaunchKernelGGL(pass_b512<0>, dim3(p->N1 / 4, (unsigned)pairs), dim3(kThreads), lds_b512, s, a);
-    else
-        hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, (unsigned)pairs), dim3(kThreads), lds_b, s, a);
+    launch_pass_b<0>(p, (unsigned)pairs, a, s);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
     return hipGetLastError();
@@ -623,13 +670,8 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.out_d = d_out_interleaved;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
-    const size_t lds_b = 2 * (size_t)p->N2 * sizeof(double2);
-    const size_t lds_b512 = (4 + 1) * 512 * sizeof(double2);
     hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
-    if (use_b512(p))
-        hipLaunchKernelGGL(pass_b512<0>, dim3(p->N1 / 4, 1), dim3(kThreads), lds_b512, s, a);
-    else
-        hipLaunchKernelGGL(pass_b<0>, dim3(p->N1, 1), dim3(kThreads), lds_b, s, a);
+    launch_pass_b<0>(p, 1, a, s);
     hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
     hipLaunchKernelGGL(pass_d_live, dim3((unsigned)((p->n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
