@@ -70,3 +70,11 @@ def test_degenerate_and_random_soup(checker, tmp_path):
     tv[:50, 3:6] = tv[:50, 0:3]  # degenerate (zero-area) triangles
     tv[50:100, 1::3] = 1.0       # triangles in one plane y = 1
     run(checker, tv, tmp_path, n_rays=800)
+
+
+@pytest.mark.parametrize("k", ["0", "1", "7", "100000"])
+def test_breadth_first_renumbering(checker, tmp_path, k):
+    """bfs_prefix_order (the scene-tree numbering arx_set_scene uses): the first k inner nodes
+    in breadth-first order, the tree still valid and closest hits still exact (k = 100000:
+    the whole tree renumbered)."""
+    run(checker, cylinders_scene(seed=11), tmp_path, n_rays=600, env={"BFS_K": k})

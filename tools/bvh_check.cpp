@@ -2,7 +2,8 @@
 //
 // For a triangle soup (raw f32, 9 per triangle) it builds the default tree (arx_bvh.cpp: SBVH
 // with spatial splits), its coded copy and the 16-bit quantized copy, and checks:
-//   1. structure (validate_bvh) and that every triangle is referenced by some leaf;
+//   1. structure (validate_bvh) and that every triangle is referenced by some leaf, after the
+//      breadth-first renumbering of the top nodes (bfs_prefix_order, as arx_set_scene);
 //   2. every quantized child box contains its f32 box (outward rounding), in exact arithmetic;
 //   3. octant copies swap exactly the lo / hi halves of the negative axes;
 //   4. closest hits of random rays through the f32 tree and through the dequantized tree equal
@@ -134,6 +135,20 @@ int main(int argc, char** argv) {
     std::fclose(f);
     BvhBuild b;
     build_bvh(tv.data(), nullptr, 0.5f, n, 0, b);
+    // renumbered as arx_set_scene does: the first k inner nodes in breadth-first order
+    const size_t k_bfs = std::getenv("BFS_K") ? (size_t)std::atol(std::getenv("BFS_K")) : 1023;
+    bfs_prefix_order(b, k_bfs);
+    if (b.root.count == 0) {
+        std::vector<int32_t> order{b.root.ref};
+        for (size_t h = 0; h < order.size() && order.size() < k_bfs; ++h)
+            for (int c = 0; c < 2 && order.size() < k_bfs; ++c)
+                if (b.nodes[(size_t)order[h]].d[2 + c] == 0) order.push_back(b.nodes[(size_t)order[h]].d[c]);
+        for (size_t i = 0; i < order.size(); ++i)
+            if (order[i] != (int32_t)i) {
+                std::printf("FAIL breadth-first prefix: position %zu holds node %d\n", i, order[i]);
+                return 1;
+            }
+    }
     // the kernel's two-level layout: node 0 = top (scene root, empty receiver)
     relocate_bvh(b, 1, 0);
     std::vector<BvhNode> nodes{make_node(b.root, empty_child())};
