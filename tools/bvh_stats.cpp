@@ -151,7 +151,8 @@ static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Sta
     while (!stack.empty()) {
         auto [tn0, code] = stack.back();
         stack.pop_back();
-        if (tn0 > best) continue;
+        static const bool nocull = std::getenv("NOCULL") != nullptr;  // the GPU stack keeps no distances
+        if (tn0 > best && !nocull) continue;
         if (code < 0) {
             const int v = -code - 1, first = v >> 4, cnt = v & 15;
             st.leaves += 1;
