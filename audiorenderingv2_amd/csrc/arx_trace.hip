@@ -2286,11 +2286,15 @@ template <typename K>
 int persistent_grid(K kernel, int block, uint64_t n_rays, int cus) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
-    const uint64_t want = (n_rays + block - 1) / block;
+    uint64_t want = (n_rays + block - 1) / block;
     uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
-    if (const char* f = getenv("ARX_GRID_PCT")) {  // design experiments: a smaller persistent grid
-        const int pct = atoi(f);
-        if (pct > 0 && pct < 100) cap = std::max<uint64_t>(1, cap * (uint64_t)pct / 100);
+    if (const char* f = getenv("ARX_GRID_PCT")) {  // design experiments: a smaller persistent grid,
+        const int pct = atoi(f);                   // or (> 100) fewer rays per lane in small launches
+        if (pct > 0 && pct < 100) {
+            cap = std::max<uint64_t>(1, cap * (uint64_t)pct / 100);
+            want = std::max<uint64_t>(1, want * (uint64_t)pct / 100);
+        }
+        if (pct > 100) want = want * (uint64_t)pct / 100;
     }
     return (int)(want < cap ? (want > 0 ? want : 1) : cap);
 }
