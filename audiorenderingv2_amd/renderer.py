@@ -116,6 +116,10 @@ class AudioRenderer:
     def setMonoOutput(self, mono: bool) -> None:
         check(lib().arx_set_mono_output(self._h, 1 if mono else 0))
 
+    def normalizeAndMergeStereoOutput(self, left, right, mono_len: int, out) -> None:
+        """Declared by the reference with an empty body (AudioRenderer.cpp:574-576): a no-op,
+        kept so callers of that API keep working (the live path zips L/R on the device)."""
+
     def set_seed(self, seed: int) -> None:
         check(lib().arx_set_seed(self._h, int(seed)))
 

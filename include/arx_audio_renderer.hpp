@@ -123,6 +123,9 @@ class AudioRenderer {
     void set_hrtf_absorption_rate(float v) { check(arx_set_hrtf_absorption_rate(h_, v)); }
     void setBasePower(float v) { check(arx_set_base_power(h_, v)); }
     void setMonoOutput(bool v) { check(arx_set_mono_output(h_, v ? 1 : 0)); }
+    // :47 -- declared by the reference, body empty (AudioRenderer.cpp:574-576); kept for source
+    // compatibility, it does nothing (the live path zips L/R in pass_d_live)
+    void normalizeAndMergeStereoOutput(double*, double*, size_t, double*) {}
 
     // full_render_cycle (AudioRenderer.cpp:790-798) minus the mutex (callers keep theirs)
     void full_render_cycle(Vec3 camera, float yaw_deg, float* audio, size_t bytes, float* outL, float* outR) {
