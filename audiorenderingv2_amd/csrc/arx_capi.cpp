@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -563,7 +564,10 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
     for (int64_t i = 0; i < 9 * n; ++i)
         if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
-    bfs_prefix_order(r->scene, 1023);  // the kernels' LDS node cache holds the top of the tree
+    {  // the top of the scene tree in breadth-first order (ARX_BFS_K: design A/B of the prefix length)
+        const char* k = std::getenv("ARX_BFS_K");
+        bfs_prefix_order(r->scene, (k && k[0]) ? (size_t)std::atoll(k) : (size_t)1023);
+    }
     relocate_bvh(r->scene, 1, 0);
     r->n_scene = n;
     r->scene_set = true;

@@ -4,6 +4,7 @@ must reproduce variant 1's IR and query count bit for bit."""
 import os
 import sys
 import time
+import zlib
 
 import numpy as np
 
@@ -38,7 +39,7 @@ def main():
             ref = (ir, st["queries"])
         same = np.array_equal(ir[0], ref[0][0]) and np.array_equal(ir[1], ref[0][1]) and st["queries"] == ref[1]
         print(f"variant {label}: median {ms[3]:.3f} ms min {ms[0]:.3f} ms  {st['queries'] / ms[3] / 1e6:.3f} Gq/s  "
-              f"identical={same}", flush=True)
+              f"identical={same}  ir_crc={zlib.crc32(ir[0].tobytes() + ir[1].tobytes()):08x}", flush=True)
         if not same:
             raise SystemExit(f"variant {v} differs from variant {variants[0]}")
 
