@@ -50,6 +50,15 @@ def test_prepared_spectra_follow_new_ir():
     assert rel_err(r.convoluteLiveInput(x), po.convolute_live_block(x, irl2, irr2)) < 1e-12
 
 
+@pytest.mark.parametrize("sr,secs", [(16000, 2), (22050, 1), (32000, 2)])
+def test_live_block_256_point_plans(sr, secs):
+    """Plans whose sub-FFTs are 256 points (M = 2^16: 16 kHz x 2 s, 22.05 kHz x 1 s) or mix
+    256-point columns with 512-point rows (M = 2^17: 32 kHz x 2 s) -- the radix-4 wave FFTs."""
+    r, (irl, irr) = live_renderer(sr=sr, secs=secs, seed=sr)
+    x = np.random.default_rng(sr).uniform(-1, 1, min(4096, sr))
+    assert rel_err(r.convoluteLiveInput(x), po.convolute_live_block(x, irl, irr)) < 1e-12
+
+
 def test_live_block_48k_and_oversize():
     r, (irl, irr) = live_renderer(sr=48000)
     x = np.random.default_rng(1).uniform(-1, 1, 4096)
