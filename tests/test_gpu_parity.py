@@ -254,6 +254,17 @@ def test_random_soup_with_degenerate_triangles(monkeypatch, variant):
     assert_same_render(r, sc, (1.5, 1.2, -0.7), 0.0, (0.0, 0.0, 0.0), s)
 
 
+@pytest.mark.parametrize("max_bounces,thres,secs", [(0, 0.0, 2), (1, 0.0, 1), (3, 0.05, 1), (64, 1e-7, 3)])
+def test_bounce_and_threshold_limits(c1_scene, max_bounces, thres, secs):
+    """Reflection-count and energy-threshold cut-offs (devicePrograms.cu:147-175, 234-236)
+    and IR lengths of 1-3 s: 0 bounces (direct sound only), early energy cut, long paths."""
+    em = (0.5, 3.0, 1.0)
+    s = RenderSettings(rays=(48, 48, 4), sample_rate=16000, ir_length_in_seconds=secs, base_power=3.62,
+                       max_bounces=max_bounces, energy_thres=thres, hrtf_absorption_rate=0.5)
+    r = make(c1_scene, (2.5, 9.9, 0.0), emitter=em, **s.__dict__)
+    assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em, s)
+
+
 def test_inverse_square_on_gpu():
     # listener on the +z (ear) axis: rays arrive through the half-spheres' domes, not through
     # the 0.058 m slot between the two halves (|z| < 0.029 in the local frame), which a
