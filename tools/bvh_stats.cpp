@@ -57,6 +57,7 @@ static bool slab(const float lo[3], const float hi[3], const Q& q, float tmax, f
 struct Stats {
     double visits = 0, tests = 0, leaves = 0, maxstack = 0;
     double shallow[8] = {};  // visits to nodes at depth <= 2 + k below the top node
+    double nhit[9] = {};     // visits by number of children hit
 };
 
 struct Tree {
@@ -177,6 +178,7 @@ static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Sta
             if (!slab(c.lo, c.hi, q, best, tn)) continue;
             hits.push_back({tn, c.count > 0 ? -(c.ref * 16 + c.count) - 1 : c.ref});
         }
+        st.nhit[std::min<size_t>(hits.size(), 8)] += 1;
         std::sort(hits.begin(), hits.end(), [](auto& a, auto& b) { return a.first > b.first; });
         for (auto& h : hits) stack.push_back(h);
         maxs = std::max(maxs, stack.size());
@@ -276,6 +278,9 @@ int main(int argc, char** argv) {
         std::printf("W=%d: %ld queries  visits %.1f  leaves %.1f  tri tests %.1f  node bytes %.0f  tri bytes %.0f  "
                     "max stack %.0f\n",
                     trees[k]->W, queries, v, lv, te, v * node_bytes[k], te * 48.0, st.maxstack);
+        std::printf("   visits by children hit: 0: %.3f 1: %.3f 2: %.3f 3+: %.3f\n", st.nhit[0] / st.visits,
+                    st.nhit[1] / st.visits, st.nhit[2] / st.visits,
+                    (st.visits - st.nhit[0] - st.nhit[1] - st.nhit[2]) / st.visits);
         if (k == 0) {
             std::printf("   share of visits at depth <=");
             for (int d = 0; d < 8; ++d) std::printf(" %d: %.3f", 2 + d, st.shallow[d] / st.visits);
