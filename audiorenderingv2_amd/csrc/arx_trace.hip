@@ -1714,7 +1714,28 @@ template <int BLOCK, int LV>
 __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Trav3& t, const int* __restrict__ stk,
                                            int lane) {
     const int v = ~t.node;
-    leaf_hits_vec<LV>(a.tris, r, v >> 4, v & 15, t.best_t, t.best_id, t.best);
+    if constexpr (LV == 0) {  // buffer loads: 32-bit offsets off a scalar base (no 64-bit address math)
+        const __amdgpu_buffer_rsrc_t trs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<TriRec*>(a.tris), (short)0, 0x7fffffff, 0x00020000);
+        const int first = v >> 4, count = v & 15;
+        for (int k = 0; k < count; ++k) {
+            const int off = (first + k) * (int)sizeof(TriRec);
+            const float4 p0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trs, off, 0, 0));
+            const float4 p1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trs, off + 16, 0, 0));
+            const float4 p2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trs, off + 32, 0, 0));
+            Hit h;
+            if (tri_test(r, p0, p1, p2, h)) {
+                const int id = __float_as_int(p1.w);
+                if (h.t < t.best_t || (h.t == t.best_t && id < t.best_id)) {
+                    t.best_t = h.t;
+                    t.best_id = id;
+                    t.best = first + k;
+                }
+            }
+        }
+    } else {
+        leaf_hits_vec<LV>(a.tris, r, v >> 4, v & 15, t.best_t, t.best_id, t.best);
+    }
     const int sp = t.sp;
     const int sp_pop = max(sp - 1, 0);
     int top = stk[sp_pop * BLOCK + lane];
@@ -2699,6 +2720,8 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 1010: return launch_v5<128, 28, 12, 12, 5, 6, 5, 1, 0, 64>(a, cus, s);
         // top of the tree in LDS (node_step8c): 64 / 32 nodes per 128-lane block, 128 per 256,
         // 320 per 640 (10 waves, 2 blocks per CU)
+        // leaf triangles through buffer loads (leaf_step8 LV = 0)
+        case 1200: return launch_v5<128, 28, 12, 12, 5, 12, 1, 0>(a, cus, s);
         case 1100: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 64>(a, cus, s);
         case 1101: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 32>(a, cus, s);
         case 1102: return launch_v5<256, 28, 12, 12, 5, 12, 6, 1, 0, 0, 128>(a, cus, s);
