@@ -176,7 +176,7 @@ def test_wide_tree_variants_match_oracle(c1_scene, conference, monkeypatch, vari
     assert st["receiver_hits"] > 0
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312", "320", "322", "323", "400", "401", "500", "501", "505", "600", "601", "606", "701", "702", "703", "706", "720", "722", "730", "732", "800", "802", "804", "810", "812", "740", "742", "745", "751", "760", "763", "767", "770", "772", "780", "781", "792", "794", "863", "861", "900", "901", "903", "905", "907", "920", "921", "923", "927", "930", "931", "778", "932", "933", "940", "941", "1000", "1002", "1004"])
+@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312", "320", "322", "323", "400", "401", "500", "501", "505", "600", "601", "606", "701", "702", "703", "706", "720", "722", "730", "732", "800", "802", "804", "810", "812", "740", "742", "745", "751", "760", "763", "767", "770", "772", "780", "781", "792", "794", "863", "861", "900", "901", "903", "905", "907", "920", "921", "923", "927", "930", "931", "778", "932", "933", "940", "941", "1000", "1002", "1004", "1101", "1103", "1200"])
 def test_kernel_variants_identical(conference, monkeypatch, variant):
     """Every trace-kernel variant (grid-stride v1, persistent v2, postponed-leaf v3 and its
     tunings, 4-/8-wide trees) produces the default kernel's histogram bit for bit."""
