@@ -1752,8 +1752,12 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 // TAIL > 0: once the wave's rays are all handed out, the shading threshold drops from THRESH to
 // (live rays) / TAIL (at least 1), so finished queries of the last rays are shaded and
 // re-issued promptly instead of waiting for THRESH idle lanes that will never come.
+// DIET = 1: fewer VGPRs held across the traversal loop, for 6 waves per SIMD: the ray state
+// (position, direction, energy, distance, depth) is kept in a per-lane 48-B record of a.stash[0]
+// from the query's setup to its shading instead of in registers, and the query / receiver /
+// miss counters are wave-level (scalar) sums of ballots.
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
-          int TAIL = 0, int LC = 0>
+          int TAIL = 0, int LC = 0, int DIET = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     constexpr int FMT = NF & 15;
     constexpr bool Q16 = FMT >= 1;
@@ -1792,6 +1796,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
     float oix = 0.f, oiy = 0.f, oiz = 0.f;
     int obase = 0;  // NF 2: byte offset of the ray's octant copy
     uint4* const lcache = reinterpret_cast<uint4*>(stk + STACK * BLOCK);
+    uint32_t wq = 0, wrx = 0, wms = 0;  // DIET: wave-level counters
+    float4* const srec = reinterpret_cast<float4*>(a.stash[0]) + (size_t)3 * (blockIdx.x * BLOCK + threadIdx.x);
     if constexpr (FMT == 6) {  // the top LC nodes (a.qcount valid ones) into LDS
         for (int i = lane; i < 2 * LC; i += BLOCK) {
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -1802,7 +1808,21 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
         __syncthreads();
     }
     while (true) {
-        if (active && !trav) {
+        if constexpr (DIET) {  // the ray state of every lane back from its record (stored at setup)
+            const float4 A = srec[0], B = srec[1], C = srec[2];
+            s.pos = make_float3(A.x, A.y, A.z);
+            s.e = A.w;
+            s.dir = make_float3(B.x, B.y, B.z);
+            s.dist = B.w;
+            s.depth = __float_as_int(C.x);
+            uint32_t rx = 0, ms = 0;
+            if (active && !trav) {
+                shade(a, s, r, t.best, rx, ms);
+                if (!wants_query(a, s)) active = false;
+            }
+            wrx += (uint32_t)__popcll(__ballot(rx != 0));
+            wms += (uint32_t)__popcll(__ballot(ms != 0));
+        } else if (active && !trav) {
             shade(a, s, r, t.best, n_rx, n_miss);
             if (!wants_query(a, s)) active = false;
         }
@@ -1833,9 +1853,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             }
             if (base + (uint64_t)cnt >= w_end && (POOL == 0 || pool)) exhausted = true;
         }
+        if constexpr (DIET) wq += (uint32_t)__popcll(__ballot(active && !trav));
         if (active && !trav) {
-            ++n_q;
+            if constexpr (!DIET) ++n_q;
             setup_ray(r, s.pos, s.dir);
+            if constexpr (DIET) {
+                srec[0] = make_float4(s.pos.x, s.pos.y, s.pos.z, s.e);
+                srec[1] = make_float4(s.dir.x, s.dir.y, s.dir.z, s.dist);
+                srec[2] = make_float4(__int_as_float(s.depth), 0.0f, 0.0f, 0.0f);
+            }
             if constexpr (Q16) {  // grid form of the slab planes (node_step7 Q16)
                 oix = (r.o[0] - a.qgrid.origin[0]) * r.inv[0];
                 oiy = (r.o[1] - a.qgrid.origin[1]) * r.inv[1];
@@ -1900,7 +1926,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
             }
         }
     }
-    flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+    if constexpr (DIET) {
+        const bool l0 = (lane & 63) == 0;
+        flush_counters(a, l0 ? wq : 0u, l0 ? wrx : 0u, l0 ? wms : 0u, overflow, lane);
+    } else {
+        flush_counters(a, n_q, n_rx, n_miss, overflow, lane);
+    }
 }
 
 // ---------------------------------------------------------------- wide tree (v4) ---
@@ -2415,7 +2446,7 @@ hipError_t launch_w(TraceArgs a, int cus, hipStream_t s) {
 // v5 launcher: direction pre-pass + static per-wave ranges; trees deeper than the LDS stack
 // take the spill-stack v3 kernel, quantized variants without a usable grid the f32 nodes.
 template <int BLOCK, int STACK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int NF, int LV = 1, int POOL = 0,
-          int TAIL = 0, int LC = 0>
+          int TAIL = 0, int LC = 0, int DIET = 0>
 hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
     if constexpr ((NF & 15) == 5) {  // 4-wide quantized: without its grid copy, the binary steps
         if (!args.qwnodes) return launch_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, 12, 1, LV, POOL, TAIL>(args, cus, s);
@@ -2437,8 +2468,10 @@ hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
         const hipError_t e = hipMemsetAsync(a.counters + 4, 0, sizeof(unsigned long long), s);  // pool cursor
         if (e != hipSuccess) return e;
     }
-    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL, LC>;
+    auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL, LC, DIET>;
     const int grid = persistent_grid(k, BLOCK, n_rays, cus);
+    if (DIET && (!a.stash[0] || (uint64_t)grid * BLOCK > a.stash_cap))  // one ray-state record per lane
+        return launch_v5<128, 28, 12, 12, 5, 12, 1>(args, cus, s);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
 }
@@ -2722,6 +2755,11 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         // 320 per 640 (10 waves, 2 blocks per CU)
         // leaf triangles through buffer loads (leaf_step8 LV = 0)
         case 1200: return launch_v5<128, 28, 12, 12, 5, 12, 1, 0>(a, cus, s);
+        // ray state in memory + scalar counters (DIET): 6 waves per SIMD with a 26-entry stack
+        // (trees deeper than 25 take the spill-stack kernel), or 5 with the default stack
+        case 1300: return launch_v5<128, 26, 12, 12, 6, 12, 1, 1, 0, 0, 0, 1>(a, cus, s);
+        case 1301: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 0, 0, 1>(a, cus, s);
+        case 1302: return launch_v5<128, 26, 12, 12, 6, 8, 1, 1, 0, 0, 0, 1>(a, cus, s);
         case 1100: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 64>(a, cus, s);
         case 1101: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 32>(a, cus, s);
         case 1102: return launch_v5<256, 28, 12, 12, 5, 12, 6, 1, 0, 0, 128>(a, cus, s);
