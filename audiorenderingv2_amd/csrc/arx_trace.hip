@@ -1752,7 +1752,7 @@ __device__ __forceinline__ void leaf_step8(const TraceArgs& a, const Ray& r, Tra
 // TAIL > 0: once the wave's rays are all handed out, the shading threshold drops from THRESH to
 // (live rays) / TAIL (at least 1), so finished queries of the last rays are shaded and
 // re-issued promptly instead of waiting for THRESH idle lanes that will never come.
-// DIET = 1: fewer VGPRs held across the traversal loop, for 6 waves per SIMD: the ray state
+// DIET = 2: only the counters below.  DIET = 1: fewer VGPRs held across the traversal loop, for 6 waves per SIMD: the ray state
 // (position, direction, energy, distance, depth) is kept in a per-lane 48-B record of a.stash[0]
 // from the query's setup to its shading instead of in registers, and the query / receiver /
 // miss counters are wave-level (scalar) sums of ballots.
@@ -1808,7 +1808,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
         __syncthreads();
     }
     while (true) {
-        if constexpr (DIET) {  // the ray state of every lane back from its record (stored at setup)
+        if constexpr (DIET == 2) {  // scalar counters only
+            uint32_t rx = 0, ms = 0;
+            if (active && !trav) {
+                shade(a, s, r, t.best, rx, ms);
+                if (!wants_query(a, s)) active = false;
+            }
+            wrx += (uint32_t)__popcll(__ballot(rx != 0));
+            wms += (uint32_t)__popcll(__ballot(ms != 0));
+        } else if constexpr (DIET == 1) {  // the ray state of every lane back from its record (stored at setup)
             const float4 A = srec[0], B = srec[1], C = srec[2];
             s.pos = make_float3(A.x, A.y, A.z);
             s.e = A.w;
@@ -1857,7 +1865,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel_v5(TraceArgs a) {
         if (active && !trav) {
             if constexpr (!DIET) ++n_q;
             setup_ray(r, s.pos, s.dir);
-            if constexpr (DIET) {
+            if constexpr (DIET == 1) {
                 srec[0] = make_float4(s.pos.x, s.pos.y, s.pos.z, s.e);
                 srec[1] = make_float4(s.dir.x, s.dir.y, s.dir.z, s.dist);
                 srec[2] = make_float4(__int_as_float(s.depth), 0.0f, 0.0f, 0.0f);
@@ -2470,7 +2478,7 @@ hipError_t launch_v5(const TraceArgs& args, int cus, hipStream_t s) {
     }
     auto k = trace_kernel_v5<BLOCK, STACK, THRESH, LEAF_THRESH, MINW, NSTEPS, NF, LV, POOL, TAIL, LC, DIET>;
     const int grid = persistent_grid(k, BLOCK, n_rays, cus);
-    if (DIET && (!a.stash[0] || (uint64_t)grid * BLOCK > a.stash_cap))  // one ray-state record per lane
+    if (DIET == 1 && (!a.stash[0] || (uint64_t)grid * BLOCK > a.stash_cap))  // one ray-state record per lane
         return launch_v5<128, 28, 12, 12, 5, 12, 1>(args, cus, s);
     hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), 0, s, a);
     return hipGetLastError();
@@ -2760,6 +2768,7 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s) {
         case 1300: return launch_v5<128, 26, 12, 12, 6, 12, 1, 1, 0, 0, 0, 1>(a, cus, s);
         case 1301: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 0, 0, 1>(a, cus, s);
         case 1302: return launch_v5<128, 26, 12, 12, 6, 8, 1, 1, 0, 0, 0, 1>(a, cus, s);
+        case 1303: return launch_v5<128, 28, 12, 12, 5, 12, 1, 1, 0, 0, 0, 2>(a, cus, s);  // scalar counters only
         case 1100: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 64>(a, cus, s);
         case 1101: return launch_v5<128, 28, 12, 12, 5, 12, 6, 1, 0, 0, 32>(a, cus, s);
         case 1102: return launch_v5<256, 28, 12, 12, 5, 12, 6, 1, 0, 0, 128>(a, cus, s);
