@@ -114,6 +114,7 @@ SIGNATURES = {
     "arx_prepare_ir_spectra": (C.c_int, [_P, C.c_int]),
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
+    "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
     # input formats (host only)
     "arx_model_load_obj": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(_P)]),
     "arx_model_free": (None, [_P]),

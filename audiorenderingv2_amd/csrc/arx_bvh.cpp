@@ -538,25 +538,7 @@ struct SpatialBuilder {
 }  // namespace
 
 BuildParams& build_params() {
-    static BuildParams p = [] {
-        BuildParams q;
-        // design experiments: ARX_SBVH=alpha[,budget[,bins[,leaf_max[,trav[,isect[,max_depth]]]]]]
-        // (alpha 0 = object splits only)
-        if (const char* e = std::getenv("ARX_SBVH")) {
-            float alpha = 0.0f, budget = q.spatial_budget, trav = q.trav_cost, isect = q.isect_cost;
-            int bins = q.bins, leaf = q.leaf_max, depth = q.max_depth;
-            const int got = std::sscanf(e, "%f,%f,%d,%d,%f,%f,%d", &alpha, &budget, &bins, &leaf, &trav, &isect, &depth);
-            q.spatial = got >= 1 && alpha > 0.0f;
-            if (q.spatial) q.spatial_alpha = alpha;
-            if (got >= 2) q.spatial_budget = budget;
-            if (got >= 3 && bins > 1 && bins <= kMaxBins) q.bins = bins;
-            if (got >= 4 && leaf >= 1 && leaf <= 15) q.leaf_max = leaf;
-            if (got >= 5 && trav > 0.0f) q.trav_cost = trav;
-            if (got >= 6 && isect > 0.0f) q.isect_cost = isect;
-            if (got >= 7 && depth >= 8 && depth < kMaxBuildDepth) q.max_depth = depth;
-        }
-        return q;
-    }();
+    static BuildParams p;  // production defaults; design tools (tools/bvh_*.cpp) edit it before building
     return p;
 }
 
@@ -681,283 +663,6 @@ void bfs_prefix_order(BvhBuild& b, size_t k) {
     b.root.ref = map[(size_t)b.root.ref];
 }
 
-namespace {
-
-ChildRef child_of(const BvhNode& n, int c) {
-    ChildRef r;
-    const float* ab = c == 0 ? n.a : n.b;
-    r.lo[0] = ab[0];
-    r.hi[0] = ab[1];
-    r.lo[1] = ab[2];
-    r.hi[1] = ab[3];
-    r.lo[2] = n.c[2 * c];
-    r.hi[2] = n.c[2 * c + 1];
-    r.ref = n.d[c];
-    r.count = n.d[2 + c];
-    return r;
-}
-
-float child_area(const ChildRef& c) {
-    const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
-    return 2.0f * (dx * dy + dy * dz + dz * dx);
-}
-
-template <int W>
-void set_slot(WideNode<W>& n, int s, const ChildRef& c) {
-    n.lox[s] = c.lo[0];
-    n.hix[s] = c.hi[0];
-    n.loy[s] = c.lo[1];
-    n.hiy[s] = c.hi[1];
-    n.loz[s] = c.lo[2];
-    n.hiz[s] = c.hi[2];
-    n.ref[s] = c.ref;
-    n.cnt[s] = c.count;
-}
-
-template <int W>
-WideNode<W> empty_wide() {
-    WideNode<W> n;
-    const ChildRef e = empty_child();
-    for (int s = 0; s < W; ++s) set_slot(n, s, e);
-    return n;
-}
-
-template <int W>
-struct Collapser {
-    const BvhBuild* b;
-    int32_t bin_offset;
-    std::vector<WideNode<W>> nodes;
-    int depth = 0;
-
-    void expand(const ChildRef& inner, std::vector<ChildRef>& kids) const {
-        const BvhNode& n = b->nodes[(size_t)(inner.ref - bin_offset)];
-        for (int c = 0; c < 2; ++c) {
-            ChildRef k = child_of(n, c);
-            if (k.count >= 0) kids.push_back(k);
-        }
-    }
-
-    int32_t emit(const ChildRef& inner, int level) {
-        depth = std::max(depth, level);
-        std::vector<ChildRef> kids;
-        expand(inner, kids);
-        while ((int)kids.size() < W) {
-            int best = -1;
-            float best_area = -1.0f;
-            for (size_t i = 0; i < kids.size(); ++i) {
-                if (kids[i].count != 0) continue;
-                const float a = child_area(kids[i]);
-                if (a > best_area) {
-                    best_area = a;
-                    best = (int)i;
-                }
-            }
-            if (best < 0) break;
-            const ChildRef k = kids[(size_t)best];
-            kids.erase(kids.begin() + best);
-            expand(k, kids);
-        }
-        const int32_t me = (int32_t)nodes.size();
-        nodes.push_back(empty_wide<W>());
-        WideNode<W> n = empty_wide<W>();
-        for (size_t i = 0; i < kids.size(); ++i) {
-            ChildRef c = kids[i];
-            if (c.count == 0) c.ref = emit(c, level + 1);
-            set_slot(n, (int)i, c);
-        }
-        nodes[(size_t)me] = n;
-        return me;
-    }
-};
-
-template <int W>
-void collapse_impl(const BvhBuild& b, int32_t bin_offset, int32_t wide_offset, WideBuild& out) {
-    Collapser<W> c;
-    c.b = &b;
-    c.bin_offset = bin_offset;
-    out.root = b.root;
-    out.depth = 0;
-    if (b.root.count == 0) {
-        out.root.ref = c.emit(b.root, 1);
-        out.depth = c.depth;
-    }
-    // relocate inner references to their final position
-    for (WideNode<W>& n : c.nodes)
-        for (int s = 0; s < W; ++s)
-            if (n.cnt[s] == 0) n.ref[s] += wide_offset;
-    if (out.root.count == 0) out.root.ref += wide_offset;
-    out.width = W;
-    out.count = c.nodes.size();
-    out.bytes.resize(out.count * sizeof(WideNode<W>));
-    if (out.count) std::memcpy(out.bytes.data(), c.nodes.data(), out.bytes.size());
-}
-
-template <int W>
-bool validate_wide_impl(const WideNode<W>* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
-                        const char** why) {
-    for (size_t k = 0; k < n_nodes; ++k) {
-        const size_t i = first + k;
-        for (int s = 0; s < W; ++s) {
-            const int32_t ref = nodes[k].ref[s], count = nodes[k].cnt[s];
-            if (count < 0) continue;
-            if (count > 0) {
-                if (ref < 0 || (size_t)ref + (size_t)count > n_tris) {
-                    *why = "wide leaf range out of bounds";
-                    return false;
-                }
-                if (count > 15 || ref >= (1 << 27)) {
-                    *why = "wide leaf larger than 15 triangles or beyond 2^27";
-                    return false;
-                }
-            } else if (ref <= (int64_t)i || (size_t)ref >= total_nodes) {
-                *why = "wide inner child index not after its parent";
-                return false;
-            }
-        }
-    }
-    return true;
-}
-
-// WideNode<4> -> QNode4: per axis, origin = node lo and the smallest power-of-two step with
-// 255 steps covering the node; child planes rounded outward (floor / ceil) in exact double
-// arithmetic, so every quantized box contains the child's padded box.
-QNode4 quantize4(const WideNode<4>& n) {
-    QNode4 q;
-    std::memset(&q, 0, sizeof(q));
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    bool any = false;
-    for (int s = 0; s < 4; ++s) {
-        if (n.cnt[s] < 0) continue;
-        any = true;
-        const float cl[3] = {n.lox[s], n.loy[s], n.loz[s]}, ch[3] = {n.hix[s], n.hiy[s], n.hiz[s]};
-        for (int k = 0; k < 3; ++k) {
-            lo[k] = std::min(lo[k], (double)cl[k]);
-            hi[k] = std::max(hi[k], (double)ch[k]);
-        }
-    }
-    int e[3] = {0, 0, 0};
-    for (int k = 0; k < 3; ++k) {
-        if (!any) {
-            lo[k] = hi[k] = 0.0;
-        }
-        q.origin[k] = (float)lo[k];  // a child's float coordinate: exact
-        const double ext = hi[k] - lo[k];
-        int ek = ext > 0.0 ? std::max(-100, (int)std::ceil(std::log2(ext / 255.0)) - 1) : -100;
-        while (std::ldexp(255.0, ek) < ext) ++ek;
-        e[k] = std::min(ek, 120);
-    }
-    q.exps = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
-    q.counts = 0;
-    for (int s = 0; s < 4; ++s) {
-        uint32_t cnt_byte = 0xFF;
-        if (n.cnt[s] >= 0) {
-            cnt_byte = (uint32_t)n.cnt[s];
-            const float cl[3] = {n.lox[s], n.loy[s], n.loz[s]}, ch[3] = {n.hix[s], n.hiy[s], n.hiz[s]};
-            for (int k = 0; k < 3; ++k) {
-                const double step = std::ldexp(1.0, e[k]);
-                double ql = std::floor(((double)cl[k] - (double)q.origin[k]) / step);
-                double qh = std::ceil(((double)ch[k] - (double)q.origin[k]) / step);
-                ql = std::max(0.0, std::min(255.0, ql));
-                qh = std::max(0.0, std::min(255.0, qh));
-                q.q[2 * k] |= (uint32_t)ql << (8 * s);
-                q.q[2 * k + 1] |= (uint32_t)qh << (8 * s);
-            }
-        }
-        q.counts |= cnt_byte << (8 * s);
-        q.ref[s] = n.cnt[s] >= 0 ? n.ref[s] : 0;
-    }
-    return q;
-}
-
-void to_q4(WideBuild& out) {
-    const WideNode<4>* w = reinterpret_cast<const WideNode<4>*>(out.bytes.data());
-    std::vector<uint8_t> bytes(out.count * sizeof(QNode4));
-    QNode4* q = reinterpret_cast<QNode4*>(bytes.data());
-    for (size_t i = 0; i < out.count; ++i) q[i] = quantize4(w[i]);
-    out.bytes.swap(bytes);
-    out.width = kWideQ4;
-}
-
-bool validate_q4(const QNode4* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
-                 const char** why) {
-    for (size_t k = 0; k < n_nodes; ++k) {
-        const size_t i = first + k;
-        for (int s = 0; s < 4; ++s) {
-            const uint32_t c = (nodes[k].counts >> (8 * s)) & 0xFF;
-            const int32_t ref = nodes[k].ref[s];
-            if (c == 0xFF) continue;
-            if (c > 15) {
-                *why = "q4 leaf larger than 15 triangles";
-                return false;
-            }
-            if (c > 0) {
-                if (ref < 0 || (size_t)ref + c > n_tris || ref >= (1 << 27)) {
-                    *why = "q4 leaf range out of bounds";
-                    return false;
-                }
-            } else if (ref <= (int64_t)i || (size_t)ref >= total_nodes) {
-                *why = "q4 inner child index not after its parent";
-                return false;
-            }
-        }
-        const uint32_t ex = nodes[k].exps;
-        for (int a = 0; a < 3; ++a) {
-            const int be = (int)((ex >> (8 * a)) & 0xFF);
-            if (be < 1 || be > 254) {
-                *why = "q4 exponent out of range";
-                return false;
-            }
-        }
-    }
-    return true;
-}
-
-}  // namespace
-
-size_t wide_node_bytes(int width) {
-    if (width == kWideQ4) return sizeof(QNode4);
-    return width == 8 ? sizeof(WideNode<8>) : sizeof(WideNode<4>);
-}
-
-void collapse_bvh(const BvhBuild& b, int32_t bin_offset, int width, int32_t wide_offset, WideBuild& out) {
-    if (width == 8) {
-        collapse_impl<8>(b, bin_offset, wide_offset, out);
-    } else {
-        collapse_impl<4>(b, bin_offset, wide_offset, out);
-        if (width == kWideQ4) to_q4(out);
-    }
-}
-
-void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<uint8_t>& out) {
-    out.resize(wide_node_bytes(width));
-    if (width == kWideQ4) {
-        WideNode<4> n = empty_wide<4>();
-        set_slot(n, 0, a);
-        set_slot(n, 1, b);
-        const QNode4 q = quantize4(n);
-        std::memcpy(out.data(), &q, sizeof(q));
-    } else if (width == 8) {
-        WideNode<8> n = empty_wide<8>();
-        set_slot(n, 0, a);
-        set_slot(n, 1, b);
-        std::memcpy(out.data(), &n, sizeof(n));
-    } else {
-        WideNode<4> n = empty_wide<4>();
-        set_slot(n, 0, a);
-        set_slot(n, 1, b);
-        std::memcpy(out.data(), &n, sizeof(n));
-    }
-}
-
-bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
-                   const char** why) {
-    if (width == kWideQ4)
-        return validate_q4(reinterpret_cast<const QNode4*>(nodes), first, n_nodes, total_nodes, n_tris, why);
-    if (width == 8)
-        return validate_wide_impl(reinterpret_cast<const WideNode<8>*>(nodes), first, n_nodes, total_nodes, n_tris, why);
-    return validate_wide_impl(reinterpret_cast<const WideNode<4>*>(nodes), first, n_nodes, total_nodes, n_tris, why);
-}
-
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why) {
     return validate_bvh_range(nodes, 0, n_nodes, n_nodes, n_tris, why);
 }
@@ -1061,44 +766,6 @@ bool quantize_nodes16(const BvhNode* coded, size_t n, const QGrid& g, QNode2* ou
                 out[i].c[c].q[k] = ql | (qh << 16);
             }
             out[i].c[c].code = b.d[c];
-        }
-    }
-    return true;
-}
-
-void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out) {
-    for (size_t i = 0; i < n; ++i) {
-        QNode2 q = in[i];
-        for (int c = 0; c < 2; ++c)
-            for (int k = 0; k < 3; ++k)
-                if ((octant >> k) & 1) {
-                    const uint32_t w = q.c[c].q[k];
-                    q.c[c].q[k] = (w >> 16) | (w << 16);
-                }
-        out[i] = q;
-    }
-}
-
-bool quantize_wide16(const WideNode<4>* in, size_t n, const QGrid& g, QWide4* out) {
-    for (size_t i = 0; i < n; ++i) {
-        const WideNode<4>& w = in[i];
-        for (int c = 0; c < 4; ++c) {
-            const float lo[3] = {w.lox[c], w.loy[c], w.loz[c]};
-            const float hi[3] = {w.hix[c], w.hiy[c], w.hiz[c]};
-            const int32_t ref = w.ref[c], cnt = w.cnt[c];
-            const bool empty = cnt < 0;
-            for (int k = 0; k < 3; ++k) {
-                uint32_t ql = 1, qh = 0;  // empty: the slab between planes 0 and 1
-                if (!empty) {
-                    if (!(lo[k] <= hi[k])) return false;
-                    const int64_t l = q_lo(g, k, lo[k]), h = q_hi(g, k, hi[k]);
-                    if (l < 0 || h > 65535) return false;
-                    ql = (uint32_t)l;
-                    qh = (uint32_t)h;
-                }
-                out[i].c[c].q[k] = ql | (qh << 16);
-            }
-            out[i].c[c].code = empty ? kEmptyChildCode : cnt == 0 ? ref : ~(ref * 16 + cnt);
         }
     }
     return true;

@@ -43,6 +43,8 @@ struct BuildParams {
     int max_depth = 26;
     int threads = 8;  // top-level subtrees built concurrently (spatial builder)
 };
+// Process-wide parameters: production defaults, never read from the environment; design tools
+// (tools/bvh_stats.cpp, tools/bvh_check.cpp) edit the struct before building.
 BuildParams& build_params();
 
 // tri_v: n*9 floats, tri_abs: n floats (may be nullptr -> absorption_fill).
@@ -53,7 +55,7 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
 // Renumber the nodes so the first k inner nodes in breadth-first order from the root take
 // indices 0..k-1 (the rest keep their order, so parents still precede their children): the
-// trace kernel keeps the top of the scene tree in LDS (trace_kernel_v5 LCACHE).
+// top levels of the scene tree share cache lines.
 void bfs_prefix_order(BvhBuild& b, size_t k);
 BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
 ChildRef empty_child();
@@ -80,32 +82,4 @@ bool qgrid_contains(const QGrid& g, const float lo[3], const float hi[3]);
 // 0.1 step (for the kernel's f32 slab arithmetic, see arx_trace.hip node_step7);
 // empty children become a one-step box at the grid corner.  False if a box leaves the grid.
 bool quantize_nodes16(const BvhNode* coded, size_t n, const QGrid& g, QNode2* out);
-// Octant copy of quantized nodes for rays whose direction has sign bits `octant` (bit k set:
-// negative component k): every axis word is (near | far << 16), i.e. lo and hi swapped on the
-// negative axes, so the slab test needs no min/max.  Octant 0 is the plain layout.
-void octant_nodes16(const QNode2* in, size_t n, int octant, QNode2* out);
-// Quantized coded copy of WideNode<4> nodes on the grid (as quantize_nodes16); false if a box
-// leaves the grid.
-bool quantize_wide16(const WideNode<4>* in, size_t n, const QGrid& g, QWide4* out);
-
-// Wide tree (W = 4 or 8) collapsed from a binary build, as raw WideNode<W> bytes.
-struct WideBuild {
-    int width = 0;
-    std::vector<uint8_t> bytes;  // n * sizeof(WideNode<W>)
-    size_t count = 0;
-    ChildRef root;               // inner: wide node index (after relocation)
-    int depth = 0;               // wide levels on the longest root path
-};
-size_t wide_node_bytes(int width);
-// Collapse `b` (its inner refs offset by bin_offset) into W-wide nodes numbered from
-// wide_offset; leaf triangle ranges are shared with the binary layout.  Each wide node takes
-// the binary children of largest surface area first (Wald et al. 2008 style collapse).
-void collapse_bvh(const BvhBuild& b, int32_t bin_offset, int width, int32_t wide_offset, WideBuild& out);
-// Wide top node: slot 0 = scene root, slot 1 = receiver root.
-void make_wide_top(int width, const ChildRef& a, const ChildRef& b, std::vector<uint8_t>& out);
-// Checks nodes [first, first + n_nodes) of a wide array of total_nodes nodes (`nodes` points
-// at node `first`): inner children after their parent and in range, leaf ranges in range.
-bool validate_wide(int width, const uint8_t* nodes, size_t first, size_t n_nodes, size_t total_nodes, size_t n_tris,
-                   const char** why);
-
 }  // namespace arx

@@ -52,10 +52,8 @@ arx_status fail(arx_status s, const char* fmt, ...) {
 // shared with arx_io.cpp so the loaders report through arx_last_error()
 void arx_set_last_error(const std::string& m) { g_last_error = m; }
 
-// device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4] ray cursor
-// [6..7] parked-ray counts of the phased launches, [8..15] utilisation counters of the
-// instrumented trace variant (98)
-constexpr int kCounters = 16;
+// device counters: [0] queries [1] receiver hits [2] misses [3] error flag
+constexpr int kCounters = 8;
 
 struct arx_renderer {
     arx_config cfg;
@@ -79,31 +77,21 @@ struct arx_renderer {
     bool scene_set = false;
 
     // device
-    BvhNode* d_nodes = nullptr;
-    BvhNode* d_cnodes = nullptr;  // coded copy (code_nodes), same indices
-    QNode2* d_qnodes = nullptr;   // 16-bit quantized copies of d_cnodes: 8 octants x nodes_cap
+    BvhNode* d_cnodes = nullptr;  // coded copy of the tree (code_nodes): the f32 fallback
+    QNode2* d_qnodes = nullptr;   // 16-bit quantized copy of d_cnodes (same indices): the default
     QGrid qgrid{};
     bool qgrid_set = false;
-    bool q_valid = false;         // d_qnodes (octant 0) matches the tree: the receiver is on the grid
-    bool qoct_valid = false;      // octants 1..7 too (uploaded only for the octant kernel variants)
+    bool q_valid = false;         // d_qnodes matches the tree: the receiver is on the grid
     std::vector<QNode2> qtop_h, qscene_h, qrecv_h;  // host images of the quantized parts
     size_t nodes_cap = 0;
     TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
-    // wide tree for trace_width() > 2 (collapsed from the binary builds above)
-    int wide_w = 0;
-    WideBuild scene_w, recv_w;
-    uint8_t* d_wnodes = nullptr;
-    QWide4* d_qwnodes = nullptr;  // quantized copy of d_wnodes (4-wide variants 1000+)
-    bool qw_valid = false;
-    uint32_t qgrid_gen = 0, qw_gen = ~0u;  // grid version / the version d_qwnodes was made on
-    size_t wnodes_cap = 0;  // bytes
-    int32_t* d_spill = nullptr;
-    size_t spill_cap = 0;   // int32 entries
-    int32_t stack_need = 0;
-    uint8_t* d_stash = nullptr;  // phased-launch ray stash (2 x lanes x 48 B)
-    void* d_dirs = nullptr;      // direction pre-pass (float4 per ray of the largest trace call)
+    int32_t* d_gstack = nullptr;  // global traversal stack for trees deeper than the LDS stack
+    size_t gstack_cap = 0;        // int32 entries
+    void* d_dirs = nullptr;       // direction pre-pass (float4 per ray of the largest trace call)
     uint64_t dirs_cap = 0;
+    bool force_global_stack = false;  // arx_debug_set_trace_path
+    bool force_f32_nodes = false;
     unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
     unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
     unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
@@ -180,80 +168,8 @@ void place_vertices(const float* local, int64_t n_vertices, float x, float y, fl
     }
 }
 
-// Wide-tree image of the current scene + receiver: [top | scene | receiver] WideNode<W>s,
-// re-collapsed only for the parts that changed; the spill stack is sized for the tree.
-arx_status ensure_wide(arx_renderer* r, bool scene_changed, bool recv_changed) {
-    const int W = trace_width();
-    if (W <= 2) return ARX_OK;
-    const size_t nb = wide_node_bytes(W);
-    bool scene_new = scene_changed || r->wide_w != W;
-    if (scene_new) collapse_bvh(r->scene, 1, W, 1, r->scene_w);
-    const bool recv_new = scene_new || recv_changed;
-    if (recv_new)
-        collapse_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), W, 1 + (int32_t)r->scene_w.count, r->recv_w);
-    r->wide_w = W;
-    const size_t total = 1 + r->scene_w.count + r->recv_w.count;
-    const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
-    if (total * nb > r->wnodes_cap) {
-        if (r->d_wnodes) ARX_HIP(hipFree(r->d_wnodes));
-        if (r->d_qwnodes) ARX_HIP(hipFree(r->d_qwnodes));
-        r->d_wnodes = nullptr;
-        r->d_qwnodes = nullptr;
-        const size_t cap = (total + 256) * nb;
-        ARX_HIP(hipMalloc(&r->d_wnodes, cap));
-        if (W == 4) ARX_HIP(hipMalloc(&r->d_qwnodes, (total + 256) * sizeof(QWide4)));
-        r->wnodes_cap = cap;
-        scene_new = true;
-    }
-    const bool regrid = W == 4 && r->qw_gen != r->qgrid_gen;
-    if (!(scene_new || recv_new || regrid)) return ARX_OK;
-    const char* why = "";
-    if (scene_new && !validate_wide(W, r->scene_w.bytes.data(), 1, r->scene_w.count, total, n_tris, &why))
-        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (scene): %s", why);
-    if (!validate_wide(W, r->recv_w.bytes.data(), 1 + r->scene_w.count, r->recv_w.count, total, n_tris, &why))
-        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (receiver): %s", why);
-    std::vector<uint8_t> top;
-    make_wide_top(W, r->scene_w.root, r->recv_w.root, top);
-    if (!validate_wide(W, top.data(), 0, 1, total, n_tris, &why))
-        return fail(ARX_ERR_INTERNAL, "wide BVH validation failed (top): %s", why);
-    ARX_HIP(hipMemcpyAsync(r->d_wnodes, top.data(), nb, hipMemcpyHostToDevice, r->stream));
-    if (scene_new && r->scene_w.count)
-        ARX_HIP(hipMemcpyAsync(r->d_wnodes + nb, r->scene_w.bytes.data(), r->scene_w.bytes.size(),
-                               hipMemcpyHostToDevice, r->stream));
-    if (r->recv_w.count)
-        ARX_HIP(hipMemcpyAsync(r->d_wnodes + (1 + r->scene_w.count) * nb, r->recv_w.bytes.data(),
-                               r->recv_w.bytes.size(), hipMemcpyHostToDevice, r->stream));
-    if (W == 4 && r->d_qwnodes && r->qgrid_set) {
-        // quantized copy of the whole wide image (scene + top + receiver) on the current grid
-        std::vector<WideNode<4>> img(total);
-        std::memcpy(&img[0], top.data(), nb);
-        if (r->scene_w.count) std::memcpy(&img[1], r->scene_w.bytes.data(), r->scene_w.bytes.size());
-        if (r->recv_w.count) std::memcpy(&img[1 + r->scene_w.count], r->recv_w.bytes.data(), r->recv_w.bytes.size());
-        std::vector<QWide4> q(total);
-        r->qw_valid = quantize_wide16(img.data(), total, r->qgrid, q.data());
-        r->qw_gen = r->qgrid_gen;
-        if (r->qw_valid)
-            ARX_HIP(hipMemcpyAsync(r->d_qwnodes, q.data(), total * sizeof(QWide4), hipMemcpyHostToDevice, r->stream));
-        ARX_HIP(hipStreamSynchronize(r->stream));  // q is pageable and local
-    }
-    // worst-case stack: every level of the deepest path leaves W-1 siblings behind
-    const int depth = 1 + std::max(r->scene_w.depth, r->recv_w.depth);
-    const int fanout = (W == kWideQ4) ? 4 : W;
-    r->stack_need = (fanout - 1) * depth + 2;
-    const size_t need = (size_t)r->stack_need * trace_spill_lanes(r->cus);
-    if (need > r->spill_cap) {
-        if (r->d_spill) ARX_HIP(hipFree(r->d_spill));
-        r->d_spill = nullptr;
-        ARX_HIP(hipMalloc(&r->d_spill, need * sizeof(int32_t)));
-        r->spill_cap = need;
-    }
-    ARX_HIP(hipStreamSynchronize(r->stream));  // pageable host sources
-    return ARX_OK;
-}
-
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_set) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
-    const bool scene_changed = r->scene_dirty, recv_changed = r->recv_dirty;
     if (r->recv_dirty) {
         // receiver halves placed in world space, left then right (placeReceiver OptixModel.cpp:153-157)
         std::vector<float> tv;
@@ -273,16 +189,13 @@ arx_status ensure_device_scene(arx_renderer* r) {
     const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
     bool full = r->scene_dirty;
     if (n_nodes > r->nodes_cap) {
-        if (r->d_nodes) ARX_HIP(hipFree(r->d_nodes));
         if (r->d_cnodes) ARX_HIP(hipFree(r->d_cnodes));
         if (r->d_qnodes) ARX_HIP(hipFree(r->d_qnodes));
-        r->d_nodes = nullptr;
         r->d_cnodes = nullptr;
         r->d_qnodes = nullptr;
         size_t cap = n_nodes + 1024;
-        ARX_HIP(hipMalloc(&r->d_nodes, cap * sizeof(BvhNode)));
         ARX_HIP(hipMalloc(&r->d_cnodes, cap * sizeof(BvhNode)));
-        ARX_HIP(hipMalloc(&r->d_qnodes, 8 * cap * sizeof(QNode2)));
+        ARX_HIP(hipMalloc(&r->d_qnodes, cap * sizeof(QNode2)));
         r->nodes_cap = cap;
         full = true;
     }
@@ -318,7 +231,6 @@ arx_status ensure_device_scene(arx_renderer* r) {
         }
         r->qgrid = make_qgrid(lo, hi, grow ? 0.5 : 0.1);
         r->qgrid_set = true;
-        ++r->qgrid_gen;
     }
     if (full || r->recv_dirty || requant) {
         BvhNode top = make_node(r->scene.root, r->recv.root);
@@ -338,7 +250,6 @@ arx_status ensure_device_scene(arx_renderer* r) {
         code_nodes(&top, 1, &ctop);
         std::vector<BvhNode> cscene, crecv(r->recv.nodes.size());
         code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
-        ARX_HIP(hipMemcpyAsync(r->d_nodes, &top, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         r->qtop_h.assign(1, QNode2{});
         r->qrecv_h.assign(crecv.size(), QNode2{});
@@ -348,12 +259,9 @@ arx_status ensure_device_scene(arx_renderer* r) {
         if ((full || requant) && !r->scene.nodes.empty()) {
             cscene.resize(r->scene.nodes.size());
             code_nodes(r->scene.nodes.data(), r->scene.nodes.size(), cscene.data());
-            if (full) {
-                ARX_HIP(hipMemcpyAsync(r->d_nodes + 1, r->scene.nodes.data(),
-                                       r->scene.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
+            if (full)
                 ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
                                        hipMemcpyHostToDevice, r->stream));
-            }
             r->qscene_h.assign(cscene.size(), QNode2{});
             if (!quantize_nodes16(cscene.data(), cscene.size(), r->qgrid, r->qscene_h.data()))
                 return fail(ARX_ERR_INTERNAL, "BVH quantization failed (scene box outside the grid)");
@@ -366,8 +274,6 @@ arx_status ensure_device_scene(arx_renderer* r) {
             ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
                                    hipMemcpyHostToDevice, r->stream));
         if (!r->recv.nodes.empty()) {
-            ARX_HIP(hipMemcpyAsync(r->d_nodes + 1 + r->scene.nodes.size(), r->recv.nodes.data(),
-                                   r->recv.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
             ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
                                    crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
             if (q_ok)
@@ -378,48 +284,15 @@ arx_status ensure_device_scene(arx_renderer* r) {
             ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
                                    r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
         r->q_valid = q_ok;
-        r->qoct_valid = false;
         // the host vectors are pageable: make sure the copies are done before they can change
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
-    if (trace_octant_nodes() && r->q_valid && !r->qoct_valid) {
-        // octant copies 1..7 of the whole quantized tree (octant 0 is the plain copy)
-        std::vector<QNode2> img;
-        auto put = [&](const std::vector<QNode2>& q, size_t at, int o) -> hipError_t {
-            if (q.empty()) return hipSuccess;
-            img.resize(q.size());
-            octant_nodes16(q.data(), q.size(), o, img.data());
-            hipError_t e = hipMemcpyAsync(r->d_qnodes + (size_t)o * r->nodes_cap + at, img.data(),
-                                          q.size() * sizeof(QNode2), hipMemcpyHostToDevice, r->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(r->stream);  // img is reused
-            return e;
-        };
-        for (int o = 1; o < 8; ++o) {
-            ARX_HIP(put(r->qtop_h, 0, o));
-            ARX_HIP(put(r->qscene_h, 1, o));
-            ARX_HIP(put(r->qrecv_h, 1 + r->scene.nodes.size(), o));
-        }
-        r->qoct_valid = true;
-    }
-    arx_status st = ensure_wide(r, scene_changed || full, recv_changed);
-    if (st != ARX_OK) return st;
     r->scene_dirty = false;
     r->recv_dirty = false;
     r->stats.n_scene_tris = r->n_scene;
     r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
     r->stats.n_nodes = (int64_t)n_nodes;
     r->stats.bvh_depth = 1 + std::max(r->scene.depth, r->recv.depth);
-    if (trace_width() <= 2) {
-        // binary kernels with a short LDS stack spill deeper entries to a per-lane column
-        const size_t need = (size_t)(r->stats.bvh_depth + 1) * trace_spill_lanes(r->cus);
-        if (need > r->spill_cap) {
-            if (r->d_spill) ARX_HIP(hipFree(r->d_spill));
-            r->d_spill = nullptr;
-            r->spill_cap = 0;
-            ARX_HIP(hipMalloc(&r->d_spill, need * sizeof(int32_t)));
-            r->spill_cap = need;
-        }
-    }
     return ARX_OK;
 }
 
@@ -522,14 +395,10 @@ void arx_destroy(arx_renderer* r) {
     if (r->conv_live) conv_plan_destroy(r->conv_live);
     hipFree(r->d_live_in);
     hipFree(r->d_live_out);
-    hipFree(r->d_nodes);
     hipFree(r->d_cnodes);
     hipFree(r->d_qnodes);
     hipFree(r->d_tris);
-    hipFree(r->d_wnodes);
-    hipFree(r->d_qwnodes);
-    hipFree(r->d_spill);
-    hipFree(r->d_stash);
+    hipFree(r->d_gstack);
     hipFree(r->d_dirs);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
@@ -564,10 +433,7 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
     for (int64_t i = 0; i < 9 * n; ++i)
         if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
-    {  // the top of the scene tree in breadth-first order (ARX_BFS_K: design A/B of the prefix length)
-        const char* k = std::getenv("ARX_BFS_K");
-        bfs_prefix_order(r->scene, (k && k[0]) ? (size_t)std::atoll(k) : (size_t)1023);
-    }
+    bfs_prefix_order(r->scene, 1023);  // the top levels of the scene tree breadth-first (node locality)
     relocate_bvh(r->scene, 1, 0);
     r->n_scene = n;
     r->scene_set = true;
@@ -652,24 +518,23 @@ arx_status arx_clear_histogram(arx_renderer* r) {
 arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (ray_end < ray_begin) return fail(ARX_ERR_INVALID_ARGUMENT, "ray_end < ray_begin");
+    // global ray ids index the launch of N = x*y*z rays: energies are normalised by N and the
+    // int64 fixed point's headroom (arx_frac_bits) assumes at most N rays per histogram
+    if (ray_end > n_rays(r->cfg))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "ray_end %llu exceeds the launch's %llu rays", (unsigned long long)ray_end,
+                    (unsigned long long)n_rays(r->cfg));
     ARX_HIP(hipSetDevice(r->cfg.device));
     arx_status st = ensure_device_scene(r);
     if (st != ARX_OK) return st;
     const arx_config& c = r->cfg;
     TraceArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.nodes = r->d_nodes;
     a.cnodes = r->d_cnodes;
-    {
-        // quantized nodes only while the emitter (the one ray origin off the geometry) is on the
-        // grid: the slab arithmetic's error bound assumes origins within the grid's extent
-        const float* e = r->emitter;
-        const bool oct_ok = !trace_octant_nodes() || r->qoct_valid;
-        a.qnodes = (r->q_valid && oct_ok && qgrid_contains(r->qgrid, e, e)) ? r->d_qnodes : nullptr;
-        a.qgrid = r->qgrid;
-        a.qostride = (uint32_t)r->nodes_cap;
-        a.qcount = (uint32_t)(1 + r->scene.nodes.size() + r->recv.nodes.size());
-    }
+    // quantized nodes only while the emitter (the one ray origin off the geometry) is on the
+    // grid: the slab arithmetic's error bound assumes origins within the grid's extent
+    const float* em = r->emitter;
+    a.qnodes = (r->q_valid && !r->force_f32_nodes && qgrid_contains(r->qgrid, em, em)) ? r->d_qnodes : nullptr;
+    a.qgrid = r->qgrid;
     a.tris = r->d_tris;
     a.hist = r->hist();
     a.counters = r->d_counters;
@@ -692,37 +557,32 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.ir_len = r->ir_len;
     a.delay = (int32_t)((double)c.sample_rate * 0.00044);  // devicePrograms.cu:125
     a.is_mono = c.is_mono;
-    a.max_visits = (int32_t)std::min<size_t>(r->nodes_cap + 8, 0x7fffffff);
     a.bvh_depth = r->stats.bvh_depth;
-    a.wnodes = r->d_wnodes;
-    {
-        const float* e = r->emitter;
-        a.qwnodes = (r->qw_valid && trace_width() == 4 && qgrid_contains(r->qgrid, e, e)) ? r->d_qwnodes : nullptr;
-    }
-    a.spill = r->d_spill;
-    a.spill_lanes = trace_spill_lanes(r->cus);
-    a.stack_need = r->stack_need;
-    if (!r->d_stash) {  // parked-ray buffers of the phased launches: 48 B per lane, two of them
-        const size_t bytes = 2 * trace_spill_lanes(r->cus) * 48;
-        ARX_HIP(hipMalloc(&r->d_stash, bytes));
-    }
-    a.stash[0] = r->d_stash;
-    a.stash[1] = r->d_stash + trace_spill_lanes(r->cus) * 48;
-    a.stash_count = r->d_counters + 6;
-    a.stash_cap = trace_spill_lanes(r->cus);
-    a.pool_from = -1;
-    if (ray_end - ray_begin > r->dirs_cap) {  // direction pre-pass buffer of the refill variants
+    if (ray_end == ray_begin) return ARX_OK;
+    if (ray_end - ray_begin > r->dirs_cap) {  // direction pre-pass buffer
         if (r->d_dirs) ARX_HIP(hipFree(r->d_dirs));
         r->d_dirs = nullptr;
         r->dirs_cap = 0;
         ARX_HIP(hipMalloc(&r->d_dirs, (ray_end - ray_begin) * 16));
         r->dirs_cap = ray_end - ray_begin;
     }
-    a.dirs_buf = r->d_dirs;
-    a.dirs_cap = r->dirs_cap;
-    if (ray_end == ray_begin) return ARX_OK;
+    a.dirs = r->d_dirs;
+    const bool gstack = r->force_global_stack || a.bvh_depth + 1 > kLdsStack;
+    if (gstack) {  // trees deeper than the LDS stack: one global column of bvh_depth + 1 entries per lane
+        const size_t lanes = trace_max_lanes(r->cus);
+        const size_t need = (size_t)(a.bvh_depth + 1) * lanes;
+        if (need > r->gstack_cap) {
+            if (r->d_gstack) ARX_HIP(hipFree(r->d_gstack));
+            r->d_gstack = nullptr;
+            r->gstack_cap = 0;
+            ARX_HIP(hipMalloc(&r->d_gstack, need * sizeof(int32_t)));
+            r->gstack_cap = need;
+        }
+        a.gstack = r->d_gstack;
+        a.gstack_lanes = lanes;
+    }
     ARX_HIP(hipEventRecord(r->ev0, r->stream));
-    ARX_HIP(launch_trace(a, r->cus, r->stream));
+    ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->ev1, r->stream));
     return ARX_OK;
 }
@@ -801,7 +661,6 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, r->ev0, r->ev1) == hipSuccess) r->stats.trace_ms = ms;
     *out = r->stats;
-    if (r->h_counters[3]) return fail(ARX_ERR_INTERNAL, "trace kernel reported a BVH stack overflow");
     return ARX_OK;
 }
 
@@ -955,6 +814,13 @@ arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t 
     if (st != ARX_OK) return st;
     ARX_HIP(hipMemcpyAsync(h_out, r->d_live_out, out_len * sizeof(double), hipMemcpyDeviceToHost, r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_debug_set_trace_path(arx_renderer* r, int path) {
+    if (!r || path < 0 || path > 3) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    r->force_f32_nodes = (path & 1) != 0;
+    r->force_global_stack = (path & 2) != 0;
     return ARX_OK;
 }
 

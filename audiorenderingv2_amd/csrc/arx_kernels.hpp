@@ -8,18 +8,13 @@
 
 namespace arx {
 
-// Trace kernel (raygen + traversal + closest-hit + histogram, fused).
-int trace_block_size();
-int trace_grid_size(uint64_t n_rays, int device_cus);
-// cus = compute units of the device (grid sizing); the variant comes from ARX_TRACE_KERNEL.
-hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s);
-int trace_variant();
-// True for the variants that read the octant copies of the quantized nodes (TraceArgs::qnodes).
-bool trace_octant_nodes();
-// Node width the current variant traverses: 2 (BvhNode) or 4 / 8 (WideNode<W>, a.wnodes).
-int trace_width();
-// Upper bound on the lanes a persistent wide-tree launch uses (spill buffer columns).
-inline uint64_t trace_spill_lanes(int cus) { return (uint64_t)(cus > 0 ? cus : 256) * 2048ull; }
+// Trace kernel (raygen + traversal + closest-hit + histogram, fused) over rays
+// [a.ray_begin, a.ray_end); cus = compute units of the device (persistent grid size).
+// Quantized nodes when a.qnodes is set, else the f32 coded nodes; the global-memory stack when
+// the tree is deeper than the LDS stack or force_global_stack (a parity hook).
+hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_global_stack = false);
+// Lanes of the largest persistent trace grid (columns of the global traversal stack).
+inline uint64_t trace_max_lanes(int cus) { return (uint64_t)(cus > 0 ? cus : 256) * 2048ull; }
 // i64 histogram -> f32 IR (+ mono merge); unit = e0 * 2^-frac_bits.
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len,
                               double unit, int32_t is_mono, hipStream_t s);

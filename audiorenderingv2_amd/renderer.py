@@ -163,6 +163,11 @@ class AudioRenderer:
     def enable_experimentation(self) -> None:
         self.experimentation = True
 
+    def set_trace_path(self, path: int) -> None:
+        """Parity hook (arx_debug_set_trace_path): bit 0 forces the f32 nodes, bit 1 the
+        global-memory traversal stack; 0 = automatic."""
+        check(lib().arx_debug_set_trace_path(self.handle, int(path)))
+
     def clear_histogram(self) -> None:
         check(lib().arx_clear_histogram(self._h))
 

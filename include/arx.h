@@ -122,7 +122,8 @@ arx_status arx_render(arx_renderer* r, double* render_ms);
  * reference is single-GPU).  The histogram is 2*ir_len int64 in device memory: [L | R],
  * fixed point with unit e0*2^-frac_bits, so a sum over shards (RCCL int64 SUM) is exact. */
 arx_status arx_clear_histogram(arx_renderer* r);
-arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end); /* global ray ids */
+/* Global ray ids, ray_end <= N = x*y*z (the energy and fixed-point normalisation assume N rays). */
+arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end);
 arx_status arx_histogram_device(arx_renderer* r, int64_t** d_hist, size_t* n_elems);
 /* Accumulate into caller-owned device memory (2*ir_len int64, e.g. a torch tensor that RCCL
  * all-reduces in place); NULL restores the renderer's own buffer. */
@@ -165,10 +166,13 @@ arx_status arx_prepare_ir_spectra(arx_renderer* r, int which);
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);
-/* Raw device counters of the last trace (n <= 16): [0] queries [1] receiver hits [2] misses
- * [3] error flag [4] ray cursor; [8..14] wave-utilisation counters of the instrumented kernel
- * variant (ARX_TRACE_KERNEL=98), see arx_trace.hip. */
+/* Raw device counters of the last trace (n <= 8): [0] queries [1] receiver hits [2] misses. */
 arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
+/* Force the trace kernel's fallback paths (parity tests of the paths real scenes rarely take):
+ * bit 0 = f32 coded nodes instead of the 16-bit quantized ones (taken automatically while the
+ * emitter is off the quantization grid), bit 1 = the global-memory traversal stack (taken
+ * automatically for trees deeper than the LDS stack); 0 = automatic. */
+arx_status arx_debug_set_trace_path(arx_renderer* r, int path);
 
 /* ---- Input formats (host only, no device needed) ------------------------------------------ */
 

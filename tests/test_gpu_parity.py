@@ -155,53 +155,60 @@ def test_full_size_c3_properties(conference):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
 
 
-@pytest.mark.parametrize("variant", ["300", "307", "310", "312", "320", "323", "720", "900", "901", "920", "921", "932", "940", "1000", "1002"])
-def test_wide_tree_variants_match_oracle(c1_scene, conference, monkeypatch, variant):
-    """4- and 8-wide trees (incl. LDS-stack spill variants) against the oracle: C1 dense,
-    a listener move (receiver-only re-collapse) and an empty scene."""
-    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
+# trace paths (arx_debug_set_trace_path): 0 = the default (16-bit quantized nodes, LDS stack),
+# 1 = f32 coded nodes (taken while the emitter is off the quantization grid), 2 = global-memory
+# stack (taken by trees deeper than the LDS stack), 3 = both fallbacks
+PATHS = ["0", "1", "2", "3"]
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_trace_paths_match_oracle(c1_scene, conference, path):
+    """Every trace path against the oracle: C1 dense, the conference stand-in, a listener move
+    (receiver sub-tree only) and an empty scene."""
     s = RenderSettings(rays=(64, 64, 8), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
     em = (0.5, 3.0, 1.0)
     r = make(c1_scene, (2.5, 9.9, 0.0), emitter=em, **s.__dict__)
+    r.set_trace_path(int(path))
     assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em, s)
     s = RenderSettings(rays=(40, 40, 10), sample_rate=16000, base_power=3.62, max_bounces=8)
     r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
+    r.set_trace_path(int(path))
     assert_same_render(r, conference, CONFERENCE_LISTENER, 0.0, CONFERENCE_EMITTER, s)
     lst = (2.0, 1.4, -1.5)
     r.setSphereCenterInOptix(lst, 33.0)
     assert_same_render(r, conference, lst, 33.0, CONFERENCE_EMITTER, s)
     empty = Scene(np.zeros((0, 9), np.float32), np.zeros(0, np.float32), [])
     r = make(empty, (0.0, 0.0, 3.0), **s.__dict__)
+    r.set_trace_path(int(path))
     gl, _, st = assert_same_render(r, empty, (0.0, 0.0, 3.0), 0.0, (0.0, 0.0, 0.0), s)
     assert st["receiver_hits"] > 0
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "143", "207", "300", "307", "310", "312", "320", "322", "323", "400", "401", "500", "501", "505", "600", "601", "606", "701", "702", "703", "706", "720", "722", "730", "732", "800", "802", "804", "810", "812", "740", "742", "745", "751", "760", "763", "767", "770", "772", "780", "781", "792", "794", "863", "861", "900", "901", "903", "905", "907", "920", "921", "923", "927", "930", "931", "778", "932", "933", "940", "941", "1000", "1002", "1004", "1101", "1103", "1200"])
-def test_kernel_variants_identical(conference, monkeypatch, variant):
-    """Every trace-kernel variant (grid-stride v1, persistent v2, postponed-leaf v3 and its
-    tunings, 4-/8-wide trees) produces the default kernel's histogram bit for bit."""
+@pytest.mark.parametrize("path", ["1", "2", "3"])
+def test_trace_paths_identical_at_c3_shape(conference, path):
+    """The fallback paths produce the default path's histogram bit for bit on a 100 K-ray,
+    16-bounce, 48 kHz launch."""
     s = RenderSettings(rays=(100, 100, 10), sample_rate=48000, base_power=3.62, max_bounces=16, hrtf_absorption_rate=0.5)
     r = make(conference, CONFERENCE_LISTENER, emitter=CONFERENCE_EMITTER, **s.__dict__)
-    monkeypatch.delenv("ARX_TRACE_KERNEL", raising=False)
     r.render()
     ref, q = r.get_ir(), r.stats()["queries"]
-    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
+    r.set_trace_path(int(path))
     r.render()
     got = r.get_ir()
     assert r.stats()["queries"] == q
     assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
 
 
-@pytest.mark.parametrize("variant", ["900", "901", "921", "932", "940", "1002"])
-def test_quantized_nodes_regrid_and_fallback(c1_scene, monkeypatch, variant):
+@pytest.mark.parametrize("path", ["0", "2"])
+def test_quantized_nodes_regrid_and_fallback(c1_scene, path):
     """16-bit quantized nodes (QNode2): the grid covers scene + receiver + emitter at scene load.
     A listener moved off the grid (outside the room) re-grids once (a wider grid, full
     re-quantization); an emitter off the grid makes the launches take the f32 coded nodes.
     Every case stays bit-exact with the oracle."""
-    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
     s = RenderSettings(rays=(64, 64, 4), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
     em = (0.5, 3.0, 1.0)
     r = make(c1_scene, (2.5, 9.9, 0.0), emitter=em, **s.__dict__)
+    r.set_trace_path(int(path))
     assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em, s)
     far = (40.0, 9.0, -25.0)  # well outside the test.obj room and its grid margin
     r.setSphereCenterInOptix(far, 10.0)
@@ -213,13 +220,12 @@ def test_quantized_nodes_regrid_and_fallback(c1_scene, monkeypatch, variant):
     assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em_far, s)
 
 
-@pytest.mark.parametrize("variant", ["921", "920", "1002"])
+@pytest.mark.parametrize("path", ["0", "1"])
 @pytest.mark.parametrize("offset", [(1.0e4, -3.0e3, 5.0e3), (-2.5e5, 0.0, 1.0e5)])
-def test_room_far_from_origin(c1_scene, monkeypatch, offset, variant):
+def test_room_far_from_origin(c1_scene, offset, path):
     """The test.obj room, emitter and listener translated far from the origin: f32 slab and
     triangle arithmetic at large magnitudes (coarse ulps) and a quantization grid whose origin
-    is far away.  Quantized (921, 1002) and f32 (920) nodes stay bit-exact with the oracle."""
-    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
+    is far away.  Quantized (0) and f32 (1) nodes stay bit-exact with the oracle."""
     off = np.asarray(offset, np.float32)
     tv = (c1_scene.tri_v.reshape(-1, 3, 3) + off).reshape(-1, 9).astype(np.float32)
     far = Scene(tv, c1_scene.tri_abs, c1_scene.names)
@@ -227,18 +233,18 @@ def test_room_far_from_origin(c1_scene, monkeypatch, offset, variant):
     lst = tuple(float(v) for v in np.float32([2.5, 9.9, 0.0]) + off)
     s = RenderSettings(rays=(64, 64, 4), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
     r = make(far, lst, emitter=em, **s.__dict__)
+    r.set_trace_path(int(path))
     _, _, st = assert_same_render(r, far, lst, 0.0, em, s)
     assert st["queries"] > 16384
 
 
-@pytest.mark.parametrize("variant", ["921", "920", "778"])
-def test_random_soup_with_degenerate_triangles(monkeypatch, variant):
+@pytest.mark.parametrize("path", PATHS)
+def test_random_soup_with_degenerate_triangles(path):
     """A closed room filled with a random triangle soup: zero-area triangles, a coplanar
     stack at y = 1, exact duplicates (equal-t ties -> lowest id), and triangles through the
-    emitter's position.  Bit-exact with the oracle on the quantized, f32 and v3 kernels."""
+    emitter's position.  Bit-exact with the oracle on every trace path."""
     from audiorenderingv2_amd.scene import _box_tris
 
-    monkeypatch.setenv("ARX_TRACE_KERNEL", variant)
     rng = np.random.default_rng(17)
     room = _box_tris(np.array([[-4, -4, -4]], np.float32), np.array([[4, 4, 4]], np.float32))
     soup = rng.uniform(-3.5, 3.5, (3000, 9)).astype(np.float32)
@@ -251,6 +257,7 @@ def test_random_soup_with_degenerate_triangles(monkeypatch, variant):
     sc = Scene(tv, ta, [])
     s = RenderSettings(rays=(64, 64, 4), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
     r = make(sc, (1.5, 1.2, -0.7), emitter=(0.0, 0.0, 0.0), **s.__dict__)
+    r.set_trace_path(int(path))
     assert_same_render(r, sc, (1.5, 1.2, -0.7), 0.0, (0.0, 0.0, 0.0), s)
 
 

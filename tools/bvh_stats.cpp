@@ -1,9 +1,9 @@
 // bvh_stats -- host-side traversal statistics of the trace kernel's trees (design tool).
 //
-// Builds the production binary SAH tree (arx_bvh.cpp) and its 4-/8-wide collapses, then
-// replays closest-hit queries of bouncing rays (specular reflection, same scene) and counts
-// per query: node visits, triangle tests and bytes fetched under each layout.  Used to pick
-// node formats: the trace kernel is bound by vector-memory instruction throughput.
+// Builds the production binary SAH tree (arx_bvh.cpp), then replays closest-hit queries of
+// bouncing rays (specular reflection, same scene) and counts per query: node visits, triangle
+// tests and bytes fetched.  (The 4-/8-wide collapses it compared in round 1 are in the git
+// history at commit 62a5de6.)
 //
 //   g++ -O2 -std=c++17 -I audiorenderingv2_amd/csrc tools/bvh_stats.cpp \
 //       audiorenderingv2_amd/csrc/arx_bvh.cpp -o /tmp/bvh_stats
@@ -96,51 +96,6 @@ static Tree from_binary(const std::vector<BvhNode>& nodes, const BvhNode& top) {
     return t;
 }
 
-template <int W>
-static Tree from_wide(const std::vector<uint8_t>& top, const WideBuild& w) {
-    Tree t;
-    t.W = W;
-    t.n = 1 + w.count;
-    t.kids.resize(W * t.n);
-    auto put = [&](size_t i, const WideNode<W>& n) {
-        for (int s = 0; s < W; ++s) {
-            ChildRef& r = t.kids[W * i + s];
-            r.lo[0] = n.lox[s]; r.hi[0] = n.hix[s]; r.lo[1] = n.loy[s]; r.hi[1] = n.hiy[s];
-            r.lo[2] = n.loz[s]; r.hi[2] = n.hiz[s];
-            r.ref = n.ref[s];
-            r.count = n.cnt[s];
-        }
-    };
-    put(0, *reinterpret_cast<const WideNode<W>*>(top.data()));
-    const WideNode<W>* p = reinterpret_cast<const WideNode<W>*>(w.bytes.data());
-    for (size_t i = 0; i < w.count; ++i) put(i + 1, p[i]);
-    return t;
-}
-
-static Tree from_q4(const std::vector<uint8_t>& top, const WideBuild& w) {
-    Tree t;
-    t.W = 4;
-    t.n = 1 + w.count;
-    t.kids.resize(4 * t.n);
-    auto put = [&](size_t i, const QNode4& n) {
-        for (int s = 0; s < 4; ++s) {
-            ChildRef& r = t.kids[4 * i + s];
-            const uint32_t c = (n.counts >> (8 * s)) & 0xFF;
-            r.count = c == 0xFF ? -1 : (int)c;
-            r.ref = n.ref[s];
-            for (int k = 0; k < 3; ++k) {
-                const int e = (int)((n.exps >> (8 * k)) & 0xFF) - 127;
-                const double step = std::ldexp(1.0, e);
-                r.lo[k] = (float)(n.origin[k] + ((n.q[2 * k] >> (8 * s)) & 0xFF) * step);
-                r.hi[k] = (float)(n.origin[k] + ((n.q[2 * k + 1] >> (8 * s)) & 0xFF) * step);
-            }
-        }
-    };
-    put(0, *reinterpret_cast<const QNode4*>(top.data()));
-    const QNode4* p = reinterpret_cast<const QNode4*>(w.bytes.data());
-    for (size_t i = 0; i < w.count; ++i) put(i + 1, p[i]);
-    return t;
-}
 
 // closest hit with near-first order; returns hit tri index or -1
 static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Stats& st, float& best) {
@@ -215,21 +170,8 @@ int main(int argc, char** argv) {
     relocate_bvh(b, 1, 0);
     BvhNode top = make_node(b.root, empty_child());
     Tree t2 = from_binary(b.nodes, top);
-    WideBuild w4, w8;
-    collapse_bvh(b, 1, 4, 1, w4);
-    collapse_bvh(b, 1, 8, 1, w8);
-    std::vector<uint8_t> top4, top8;
-    make_wide_top(4, w4.root, empty_child(), top4);
-    make_wide_top(8, w8.root, empty_child(), top8);
-    Tree t4 = from_wide<4>(top4, w4), t8 = from_wide<8>(top8, w8);
-    WideBuild wq;
-    collapse_bvh(b, 1, kWideQ4, 1, wq);
-    std::vector<uint8_t> topq;
-    make_wide_top(kWideQ4, wq.root, empty_child(), topq);
-    Tree tq = from_q4(topq, wq);
     std::printf("spatial %d alpha %g budget %g: refs %zu\n", (int)bp.spatial, bp.spatial_alpha, bp.spatial_budget, b.tris.size());
-    std::printf("tris %ld  binary nodes %zu depth %d | wide4 %zu depth %d | wide8 %zu depth %d\n", n, b.nodes.size(),
-                b.depth, w4.count, w4.depth, w8.count, w8.depth);
+    std::printf("tris %ld  binary nodes %zu depth %d\n", n, b.nodes.size(), b.depth);
     t2.set_depths();
     {
         long cnt[40] = {};
@@ -239,10 +181,10 @@ int main(int argc, char** argv) {
         for (int d = 0; d < 12; ++d) std::printf(" %d:%ld", d, cum += cnt[d]);
         std::printf("\n");
     }
-    Tree* trees[4] = {&t2, &t4, &t8, &tq};
-    const double node_bytes[4] = {64, 128, 256, 64};
+    Tree* trees[1] = {&t2};
+    const double node_bytes[1] = {32};  // QNode2
     std::uniform_real_distribution<float> U(0.0f, 1.0f);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 1; ++k) {
         Stats st;
         long queries = 0;
         std::mt19937 r2(7);

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmcs
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-for v in ${VARIANTS:-0}; do
+for v in ${VARIANTS:-0}; do  # v: a tag (the library is ARX_LIB)
 for grp in "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM" \
@@ -15,7 +15,7 @@ for grp in "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_R
            "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum" \
            "TCC_HIT_sum TCC_MISS_sum"; do
   tag=v${v}_$(echo $grp | cut -d' ' -f1)
-  ARX_TRACE_KERNEL=$v timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmcs/$tag -o p -- python3 $R/tools/trace_once.py 1 > gpurun_out/pmcs/$tag.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmcs/$tag -o p -- python3 $R/tools/trace_once.py 1 > gpurun_out/pmcs/$tag.log 2>&1
   rc=$?
   echo "$tag rc=$rc" >> gpurun_out/pmcs/status.txt
   if [ $rc -ne 0 ]; then echo "pmc $tag failed rc=$rc"; tail -5 gpurun_out/pmcs/$tag.log; exit 1; fi

@@ -15,8 +15,3 @@ for grp in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_traffic_$TAG/$grp" -o p -- python3 tools/trace_once.py 2 > gpurun_out/pmc_traffic_$TAG/$grp.log 2>&1 || { echo "pmc $grp failed"; tail -5 gpurun_out/pmc_traffic_$TAG/$grp.log; exit 1; }
 done
 python tools/make_traffic.py gpurun_out/pmc_traffic_$TAG c3 gpurun_out/trace_traffic_$TAG.json
-# optional design experiment after the round: EXTRA_SBVH / EXTRA_VARIANTS
-if [ -n "$EXTRA_VARIANTS" ]; then
-  ARX_SBVH=${EXTRA_SBVH:-1e-3} timeout -k 10 300 python -u tools/trace_variants.py $EXTRA_VARIANTS > gpurun_out/extra_$TAG.log 2>&1 || { tail -20 gpurun_out/extra_$TAG.log; exit 1; }
-  cat gpurun_out/extra_$TAG.log
-fi
