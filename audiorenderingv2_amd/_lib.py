@@ -115,6 +115,27 @@ SIGNATURES = {
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
+    "arx_group_create": (C.c_int, [C.POINTER(ArxConfig), _I32, C.c_int32, C.POINTER(_P)]),
+    "arx_group_unique_id": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "arx_group_create_rank": (C.c_int, [C.POINTER(ArxConfig), C.c_int32, C.c_int32, C.c_char_p, C.c_size_t,
+                                        C.POINTER(_P)]),
+    "arx_group_destroy": (None, [_P]),
+    "arx_group_members": (C.c_int32, [_P]),
+    "arx_group_ranks": (C.c_int32, [_P]),
+    "arx_group_member": (_P, [_P, C.c_int32]),
+    "arx_group_set_scene": (C.c_int, [_P, _F, _F, C.c_int64]),
+    "arx_group_set_receiver_model": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
+    "arx_group_set_emitter": (C.c_int, [_P, C.c_float, C.c_float, C.c_float]),
+    "arx_group_set_listener": (C.c_int, [_P, C.c_float, C.c_float, C.c_float, C.c_float]),
+    "arx_group_set_thresholds": (C.c_int, [_P, C.c_float, C.c_uint32]),
+    "arx_group_set_hrtf_absorption_rate": (C.c_int, [_P, C.c_float]),
+    "arx_group_set_base_power": (C.c_int, [_P, C.c_float]),
+    "arx_group_set_mono_output": (C.c_int, [_P, C.c_int]),
+    "arx_group_set_seed": (C.c_int, [_P, C.c_uint64]),
+    "arx_group_render": (C.c_int, [_P, _D]),
+    "arx_group_synchronize": (C.c_int, [_P]),
+    "arx_group_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
+    "arx_group_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),
     # input formats (host only)
     "arx_model_load_obj": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(_P)]),
     "arx_model_free": (None, [_P]),

@@ -24,8 +24,8 @@ OBJDIR = os.path.join(PKG, "_obj")
 LIB = os.path.join(PKG, "libarx.so")
 ARCH = os.environ.get("ARX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["arx_trace.hip", "arx_conv.hip", "arx_capi.cpp", "arx_bvh.cpp", "arx_io.cpp"]
-HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp"]
+SOURCES = ["arx_trace.hip", "arx_conv.hip", "arx_capi.cpp", "arx_group.cpp", "arx_bvh.cpp", "arx_io.cpp"]
+HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp"]
 
 COMMON = [
     "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
@@ -45,44 +45,60 @@ def _newest(paths: list[str]) -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = ()) -> str:
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
     deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "arx.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
     lang = ["-x", "hip"]  # host-only TUs too: they use the HIP runtime headers
-    cmd = [hipcc(), *lang, *COMMON, "-c", src, "-o", obj]
+    cmd = [hipcc(), *lang, *COMMON, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
     return obj
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force: bool = False, verbose: bool = False, exp: str | None = None, defines: tuple[str, ...] = ()) -> str:
+    """The product libarx.so; with exp="<tag>", a design-experiment library
+    tools/experiments/lib/libarx_<tag>.so built with the given -D macros (ARX_TRACE_*,
+    ARX_LDS_STACK), loaded by tools through ARX_LIB.  The product build takes no macros."""
+    objdir, lib = OBJDIR, LIB
+    if exp:
+        objdir = os.path.join(REPO, "tools", "experiments", "obj", exp)
+        lib = os.path.join(REPO, "tools", "experiments", "lib", f"libarx_{exp}.so")
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        force = True
+    os.makedirs(objdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     if force:
-        for f in os.listdir(OBJDIR):
-            os.remove(os.path.join(OBJDIR, f))
+        for f in os.listdir(objdir):
+            os.remove(os.path.join(objdir, f))
     with cf.ThreadPoolExecutor(max_workers=min(4, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest(objs):
-        return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs, "-Wl,--no-undefined"]
+        objs = list(ex.map(lambda s: _compile(s, objdir, tuple(defines)), srcs))
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest(objs):
+        return lib
+    # RCCL for the multi-GPU groups' IR all-reduce (arx_group.cpp), from the ROCm install
+    rocm_lib = os.path.join(os.path.dirname(os.path.dirname(hipcc())), "lib")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs, "-Wl,--no-undefined",
+           f"-L{rocm_lib}", "-lrccl", f"-Wl,-rpath,{rocm_lib}"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", lib)
+    return lib
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--exp", help="design-experiment library tag (tools/experiments/lib/libarx_<tag>.so)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="macro for --exp builds")
     args = ap.parse_args(argv)
-    build(force=args.force, verbose=True)
+    if args.defines and not args.exp:
+        ap.error("-D is only for --exp builds")
+    build(force=args.force, verbose=True, exp=args.exp, defines=tuple(args.defines))
     return 0
 
 

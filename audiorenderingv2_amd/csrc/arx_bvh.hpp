@@ -40,7 +40,7 @@ struct BuildParams {
     // Depth cap of the spatial builder: once depth + log2(refs / leaf_max) reaches it, nodes are
     // split at the object median of their widest centroid axis, so every leaf sits at depth <=
     // max_depth (the kernel's 28-entry LDS stack then needs no spill path).
-    int max_depth = 26;
+    int max_depth = kLdsStack - 2;
     int threads = 8;  // top-level subtrees built concurrently (spatial builder)
 };
 // Process-wide parameters: production defaults, never read from the environment; design tools

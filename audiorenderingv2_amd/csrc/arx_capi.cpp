@@ -18,18 +18,15 @@
 #include <string>
 #include <vector>
 
-#include "../../include/arx.h"
-#include "arx_bvh.hpp"
-#include "arx_kernels.hpp"
-#include "arx_layout.hpp"
+#include "arx_internal.hpp"
 
 using namespace arx;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
-arx_status fail(arx_status s, const char* fmt, ...) {
+arx_status arx::fail(arx_status s, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -39,85 +36,10 @@ arx_status fail(arx_status s, const char* fmt, ...) {
     return s;
 }
 
-#define ARX_HIP(call)                                                                                      \
-    do {                                                                                                   \
-        hipError_t e_ = (call);                                                                            \
-        if (e_ != hipSuccess)                                                                              \
-            return fail(e_ == hipErrorOutOfMemory ? ARX_ERR_OUT_OF_MEMORY : ARX_ERR_HIP, "%s failed: %s (%s:%d)", \
-                        #call, hipGetErrorString(e_), __FILE__, __LINE__);                                 \
-    } while (0)
-
-}  // namespace
-
 // shared with arx_io.cpp so the loaders report through arx_last_error()
 void arx_set_last_error(const std::string& m) { g_last_error = m; }
 
-// device counters: [0] queries [1] receiver hits [2] misses [3] error flag
-constexpr int kCounters = 8;
-
-struct arx_renderer {
-    arx_config cfg;
-    int32_t ir_len = 0;
-    int cus = 256;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-
-    float emitter[3] = {0.f, 0.f, 0.f};
-    float center[3] = {0.f, 0.f, 0.f};
-    float yaw = 0.f;
-
-    // host scene
-    int64_t n_scene = 0;
-    BvhBuild scene;
-    std::vector<float> recv_local[2];
-    BvhBuild recv;
-    bool scene_dirty = true;
-    bool recv_dirty = true;
-    bool scene_set = false;
-
-    // device
-    BvhNode* d_cnodes = nullptr;  // coded copy of the tree (code_nodes): the f32 fallback
-    QNode2* d_qnodes = nullptr;   // 16-bit quantized copy of d_cnodes (same indices): the default
-    QGrid qgrid{};
-    bool qgrid_set = false;
-    bool q_valid = false;         // d_qnodes matches the tree: the receiver is on the grid
-    std::vector<QNode2> qtop_h, qscene_h, qrecv_h;  // host images of the quantized parts
-    size_t nodes_cap = 0;
-    TriRec* d_tris = nullptr;
-    size_t tris_cap = 0;
-    int32_t* d_gstack = nullptr;  // global traversal stack for trees deeper than the LDS stack
-    size_t gstack_cap = 0;        // int32 entries
-    void* d_dirs = nullptr;       // direction pre-pass (float4 per ray of the largest trace call)
-    uint64_t dirs_cap = 0;
-    bool force_global_stack = false;  // arx_debug_set_trace_path
-    bool force_f32_nodes = false;
-    unsigned long long* d_hist = nullptr;  // 2*ir_len (own)
-    unsigned long long* d_hist_ext = nullptr;  // caller-attached (arx_attach_histogram)
-    unsigned long long* hist() const { return d_hist_ext ? d_hist_ext : d_hist; }
-    float* d_ir = nullptr;                 // 2*ir_len: L then R
-    unsigned long long* d_counters = nullptr;
-    unsigned long long* h_counters = nullptr;  // pinned
-
-    ConvPlan* conv_live = nullptr;  // mic path plan (block = live block length)
-    bool conv_live_ir_dirty = true;
-    double* d_live_in = nullptr;
-    double* d_live_out = nullptr;
-
-    ConvPlan* conv = nullptr;
-    bool conv_ir_dirty = true;
-    float* d_conv_in = nullptr;
-    float* d_conv_out = nullptr;
-    size_t conv_cap = 0;
-
-    arx_stats stats;
-};
-
 namespace {
-
-uint64_t n_rays(const arx_config& c) {
-    return (uint64_t)(int64_t)c.rays_x * (uint64_t)(int64_t)c.rays_y * (uint64_t)(int64_t)c.rays_z;
-}
 
 float initial_energy(const arx_config& c) {
     // devicePrograms.cu:208 -- (x*y*z) is an int product in the reference
@@ -195,7 +117,10 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->d_qnodes = nullptr;
         size_t cap = n_nodes + 1024;
         ARX_HIP(hipMalloc(&r->d_cnodes, cap * sizeof(BvhNode)));
-        ARX_HIP(hipMalloc(&r->d_qnodes, cap * sizeof(QNode2)));
+#ifndef ARX_QNODES_ALLOC_FACTOR
+#define ARX_QNODES_ALLOC_FACTOR 1  // design experiments only (build.py --exp)
+#endif
+        ARX_HIP(hipMalloc(&r->d_qnodes, ARX_QNODES_ALLOC_FACTOR * cap * sizeof(QNode2)));
         r->nodes_cap = cap;
         full = true;
     }

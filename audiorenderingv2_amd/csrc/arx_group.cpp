@@ -1,0 +1,319 @@
+// arx_group.cpp -- ray-sharded multi-GPU rendering behind the C ABI (include/arx.h, arx_group_*).
+//
+// The reference renders on one GPU (deviceID 0 hard-coded, AudioRenderer.cpp:252) and has no
+// collective anywhere.  Here a group holds one renderer per GPU; rank g of G
+// traces the global ray ids [g*N/G, (g+1)*N/G) of the same N-ray launch (the Philox key is the
+// global id, so the union of shards is exactly the single-GPU launch), and ONE RCCL all-reduce
+// (int64 SUM) of the 2*ir_len fixed-point histogram over xGMI leaves the full IR on every rank:
+// exact, so the IR is bitwise independent of G.
+//
+// Two ways to form a group:
+//   arx_group_create       one process drives several GPUs (ncclCommInitAll);
+//   arx_group_create_rank  one GPU per process (torchrun-style), joined through an RCCL unique
+//                          id that rank 0 shares out of band (ncclCommInitRank).
+// A device listed more than once in arx_group_create (oversubscribing one GPU, e.g. to test the
+// sharding on a single-GPU box) cannot join an RCCL communicator twice; such a group sums its
+// histograms on that device instead (hist_add kernel) -- the same exact int64 sum.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "arx_internal.hpp"
+
+using namespace arx;
+
+struct arx_group {
+    std::vector<arx_renderer*> members;  // local members, member i = global rank rank0 + i
+    std::vector<ncclComm_t> comms;       // one per member (empty: single rank or on-device sum)
+    int32_t n_ranks = 1;
+    int32_t rank0 = 0;
+    bool device_sum = false;             // all members on one device: sum there, no RCCL
+    std::vector<hipEvent_t> traced;      // per member: its shard's trace is done
+    hipEvent_t summed = nullptr;         // member 0: the on-device sum is done
+};
+
+namespace {
+
+#define ARX_NCCL(call)                                                                            \
+    do {                                                                                          \
+        ncclResult_t e_ = (call);                                                                 \
+        if (e_ != ncclSuccess)                                                                    \
+            return fail(ARX_ERR_HIP, "%s failed: %s (%s:%d)", #call, ncclGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+void destroy_members(arx_group* g) {
+    for (ncclComm_t c : g->comms)
+        if (c) ncclCommDestroy(c);
+    g->comms.clear();
+    for (size_t i = 0; i < g->traced.size(); ++i) {
+        hipSetDevice(g->members[i]->cfg.device);
+        if (g->traced[i]) hipEventDestroy(g->traced[i]);
+    }
+    if (g->summed) {
+        hipSetDevice(g->members[0]->cfg.device);
+        hipEventDestroy(g->summed);
+    }
+    for (arx_renderer* r : g->members) arx_destroy(r);
+    g->members.clear();
+}
+
+arx_status make_members(arx_group* g, const arx_config* cfg, const int32_t* devices, int32_t n) {
+    for (int32_t i = 0; i < n; ++i) {
+        arx_config c = *cfg;
+        c.device = devices[i];
+        arx_renderer* r = nullptr;
+        arx_status st = arx_create(&c, &r);
+        if (st != ARX_OK) return st;
+        g->members.push_back(r);
+        hipEvent_t ev = nullptr;
+        ARX_HIP(hipSetDevice(c.device));
+        ARX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        g->traced.push_back(ev);
+    }
+    return ARX_OK;
+}
+
+template <typename F>
+arx_status for_all(arx_group* g, F f) {
+    if (!g) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL");
+    for (arx_renderer* r : g->members) {
+        const arx_status st = f(r);
+        if (st != ARX_OK) return st;
+    }
+    return ARX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+arx_status arx_group_create(const arx_config* cfg, const int32_t* devices, int32_t n_devices, arx_group** out) {
+    if (!out || !cfg || n_devices <= 0) return fail(ARX_ERR_INVALID_ARGUMENT, "bad group arguments");
+    *out = nullptr;
+    std::vector<int32_t> devs(n_devices);
+    for (int32_t i = 0; i < n_devices; ++i) devs[i] = devices ? devices[i] : i;
+    std::vector<int32_t> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    const bool one_device = sorted.front() == sorted.back();
+    if (!distinct && !one_device)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "a group lists distinct GPUs (RCCL) or one GPU several times, not a mix");
+    arx_group* g = new (std::nothrow) arx_group();
+    if (!g) return fail(ARX_ERR_OUT_OF_MEMORY, "host allocation failed");
+    g->n_ranks = n_devices;
+    g->rank0 = 0;
+    g->device_sum = n_devices > 1 && !distinct;
+    arx_status st = make_members(g, cfg, devs.data(), n_devices);
+    if (st == ARX_OK && g->device_sum) {
+        if (hipSetDevice(devs[0]) != hipSuccess || hipEventCreateWithFlags(&g->summed, hipEventDisableTiming) != hipSuccess)
+            st = fail(ARX_ERR_HIP, "arx_group_create: event creation failed");
+    }
+    if (st == ARX_OK && distinct) {  // RCCL even for one GPU: the same exchange path at every size
+        g->comms.assign(n_devices, nullptr);
+        const ncclResult_t e = ncclCommInitAll(g->comms.data(), n_devices, devs.data());
+        if (e != ncclSuccess) {
+            g->comms.clear();
+            st = fail(ARX_ERR_HIP, "ncclCommInitAll(%d devices) failed: %s", n_devices, ncclGetErrorString(e));
+        }
+    }
+    if (st != ARX_OK) {
+        destroy_members(g);
+        delete g;
+        return st;
+    }
+    *out = g;
+    return ARX_OK;
+}
+
+arx_status arx_group_unique_id(uint8_t* id, size_t n) {
+    if (!id || n != NCCL_UNIQUE_ID_BYTES) return fail(ARX_ERR_INVALID_ARGUMENT, "the RCCL unique id is %d bytes", NCCL_UNIQUE_ID_BYTES);
+    ncclUniqueId u;
+    ARX_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return ARX_OK;
+}
+
+arx_status arx_group_create_rank(const arx_config* cfg, int32_t n_ranks, int32_t rank, const uint8_t* id, size_t n,
+                                 arx_group** out) {
+    if (!out || !cfg || n_ranks <= 0 || rank < 0 || rank >= n_ranks || (id && n != NCCL_UNIQUE_ID_BYTES) ||
+        (n_ranks > 1 && !id))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad group rank arguments");
+    *out = nullptr;
+    arx_group* g = new (std::nothrow) arx_group();
+    if (!g) return fail(ARX_ERR_OUT_OF_MEMORY, "host allocation failed");
+    g->n_ranks = n_ranks;
+    g->rank0 = rank;
+    const int32_t dev = cfg->device;
+    arx_status st = make_members(g, cfg, &dev, 1);
+    ncclUniqueId u;
+    if (st == ARX_OK) {
+        if (id) {
+            std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+        } else if (ncclGetUniqueId(&u) != ncclSuccess) {  // a one-rank group needs no shared id
+            st = fail(ARX_ERR_HIP, "ncclGetUniqueId failed");
+        }
+    }
+    if (st == ARX_OK) {
+        g->comms.assign(1, nullptr);
+        hipSetDevice(dev);
+        const ncclResult_t e = ncclCommInitRank(&g->comms[0], n_ranks, u, rank);
+        if (e != ncclSuccess) {
+            g->comms.clear();
+            st = fail(ARX_ERR_HIP, "ncclCommInitRank(rank %d of %d) failed: %s", rank, n_ranks, ncclGetErrorString(e));
+        }
+    }
+    if (st != ARX_OK) {
+        destroy_members(g);
+        delete g;
+        return st;
+    }
+    *out = g;
+    return ARX_OK;
+}
+
+void arx_group_destroy(arx_group* g) {
+    if (!g) return;
+    for (arx_renderer* r : g->members) {
+        hipSetDevice(r->cfg.device);
+        hipStreamSynchronize(r->stream);
+    }
+    destroy_members(g);
+    delete g;
+}
+
+int32_t arx_group_members(const arx_group* g) { return g ? (int32_t)g->members.size() : 0; }
+
+int32_t arx_group_ranks(const arx_group* g) { return g ? g->n_ranks : 0; }
+
+arx_renderer* arx_group_member(arx_group* g, int32_t i) {
+    if (!g || i < 0 || i >= (int32_t)g->members.size()) return nullptr;
+    return g->members[i];
+}
+
+arx_status arx_group_set_scene(arx_group* g, const float* tri_v, const float* tri_abs, int64_t n) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_scene(r, tri_v, tri_abs, n); });
+}
+arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_v, int64_t n) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_receiver_model(r, side, tri_v, n); });
+}
+arx_status arx_group_set_emitter(arx_group* g, float x, float y, float z) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_emitter(r, x, y, z); });
+}
+arx_status arx_group_set_listener(arx_group* g, float x, float y, float z, float yaw_deg) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_listener(r, x, y, z, yaw_deg); });
+}
+arx_status arx_group_set_thresholds(arx_group* g, float energy, uint32_t max_bounces) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_thresholds(r, energy, max_bounces); });
+}
+arx_status arx_group_set_hrtf_absorption_rate(arx_group* g, float rate) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_hrtf_absorption_rate(r, rate); });
+}
+arx_status arx_group_set_base_power(arx_group* g, float p) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_base_power(r, p); });
+}
+arx_status arx_group_set_mono_output(arx_group* g, int mono) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_mono_output(r, mono); });
+}
+arx_status arx_group_set_seed(arx_group* g, uint64_t seed) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_seed(r, seed); });
+}
+
+arx_status arx_group_render(arx_group* g, double* render_ms) {
+    if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
+    const uint64_t n = n_rays(g->members[0]->cfg);
+    const size_t bins = 2 * (size_t)g->members[0]->ir_len;
+    // 1. every local member traces its shard (async on its own stream)
+    for (size_t i = 0; i < g->members.size(); ++i) {
+        arx_renderer* r = g->members[i];
+        const uint64_t rank = (uint64_t)g->rank0 + i;
+        arx_status st = arx_clear_histogram(r);
+        if (st == ARX_OK) st = arx_trace_rays(r, n * rank / (uint64_t)g->n_ranks, n * (rank + 1) / (uint64_t)g->n_ranks);
+        if (st != ARX_OK) return st;
+    }
+    // 2. the exchange step: int64 SUM of the histograms
+    if (!g->comms.empty()) {
+        ARX_NCCL(ncclGroupStart());
+        for (size_t i = 0; i < g->members.size(); ++i) {
+            arx_renderer* r = g->members[i];
+            const ncclResult_t e = ncclAllReduce(r->hist(), r->hist(), bins, ncclInt64, ncclSum, g->comms[i], r->stream);
+            if (e != ncclSuccess) {
+                ncclGroupEnd();
+                return fail(ARX_ERR_HIP, "ncclAllReduce failed: %s", ncclGetErrorString(e));
+            }
+        }
+        ARX_NCCL(ncclGroupEnd());
+    } else if (g->device_sum) {
+        arx_renderer* r0 = g->members[0];
+        ARX_HIP(hipSetDevice(r0->cfg.device));
+        for (size_t i = 1; i < g->members.size(); ++i) {
+            arx_renderer* r = g->members[i];
+            ARX_HIP(hipEventRecord(g->traced[i], r->stream));
+            ARX_HIP(hipStreamWaitEvent(r0->stream, g->traced[i], 0));
+            ARX_HIP(launch_hist_add((long long*)r0->hist(), (const long long*)r->hist(), bins, r0->stream));
+        }
+        ARX_HIP(hipEventRecord(g->summed, r0->stream));
+        for (size_t i = 1; i < g->members.size(); ++i) {
+            arx_renderer* r = g->members[i];
+            ARX_HIP(hipStreamWaitEvent(r->stream, g->summed, 0));
+            ARX_HIP(hipMemcpyAsync(r->hist(), r0->hist(), bins * sizeof(long long), hipMemcpyDeviceToDevice, r->stream));
+        }
+    }
+    // 3. every member finalises the full IR
+    for (arx_renderer* r : g->members) {
+        const arx_status st = arx_finalize_ir(r);
+        if (st != ARX_OK) return st;
+    }
+    if (render_ms) {  // the reference's window (AudioRenderer.cpp:495-518): the longest shard trace
+        double worst = 0.0;
+        for (arx_renderer* r : g->members) {
+            ARX_HIP(hipSetDevice(r->cfg.device));
+            ARX_HIP(hipEventSynchronize(r->ev1));
+            float ms = 0.f;
+            ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
+            worst = std::max(worst, (double)ms);
+        }
+        *render_ms = worst;
+    }
+    return ARX_OK;
+}
+
+arx_status arx_group_synchronize(arx_group* g) {
+    return for_all(g, [&](arx_renderer* r) -> arx_status {
+        ARX_HIP(hipSetDevice(r->cfg.device));
+        ARX_HIP(hipStreamSynchronize(r->stream));
+        return ARX_OK;
+    });
+}
+
+arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len) {
+    if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
+    return arx_copy_ir(g->members[0], h_left, h_right, ir_len);
+}
+
+arx_status arx_group_get_stats(arx_group* g, arx_stats* out) {
+    if (!g || g->members.empty() || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    arx_stats sum;
+    std::memset(&sum, 0, sizeof(sum));
+    for (arx_renderer* r : g->members) {
+        arx_stats s;
+        const arx_status st = arx_get_stats(r, &s);
+        if (st != ARX_OK) return st;
+        sum.queries += s.queries;
+        sum.receiver_hits += s.receiver_hits;
+        sum.misses += s.misses;
+        sum.trace_ms = std::max(sum.trace_ms, s.trace_ms);
+        sum.conv_ms = std::max(sum.conv_ms, s.conv_ms);
+        sum.n_scene_tris = s.n_scene_tris;
+        sum.n_receiver_tris = s.n_receiver_tris;
+        sum.n_nodes = s.n_nodes;
+        sum.bvh_depth = s.bvh_depth;
+    }
+    *out = sum;
+    return ARX_OK;
+}
+
+}  // extern "C"

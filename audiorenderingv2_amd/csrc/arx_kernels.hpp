@@ -18,6 +18,8 @@ inline uint64_t trace_max_lanes(int cus) { return (uint64_t)(cus > 0 ? cus : 256
 // i64 histogram -> f32 IR (+ mono merge); unit = e0 * 2^-frac_bits.
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len,
                               double unit, int32_t is_mono, hipStream_t s);
+// dst[i] += src[i], i < n (int64 histogram bins).
+hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hipStream_t s);
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
 
 // ---- convolution (arx_conv.hip) ----

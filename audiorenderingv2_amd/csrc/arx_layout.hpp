@@ -61,7 +61,10 @@ struct QGrid {
 // LDS traversal stack rows per lane of the trace kernel; trees with bvh_depth >= kLdsStack take
 // the global-memory stack instance of the same kernel.  The SBVH builder caps its depth at 26
 // (BuildParams::max_depth), so the production scenes always fit the LDS stack.
-constexpr int kLdsStack = 28;
+#ifndef ARX_LDS_STACK
+#define ARX_LDS_STACK 28  // design experiments only (build.py --exp); BuildParams::max_depth follows it
+#endif
+constexpr int kLdsStack = ARX_LDS_STACK;
 constexpr int kMaxBuildDepth = 62;
 constexpr int kSpeedOfSound = 343;  // devicePrograms.cu:13
 

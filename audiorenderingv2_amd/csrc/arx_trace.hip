@@ -458,6 +458,24 @@ __device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav
     t.sp = sp_pop;
 }
 
+// Highest VGPR the trace kernel claims, so that its allocation (granule 8) admits exactly
+// ARX_TRACE_WAVES waves per SIMD: 5 -> 88 VGPRs (512/88 = 5.8), 4 -> 104, 6 -> 80.  Every wave of
+// a persistent launch owns an equal share of the rays, so a SIMD holding one wave more than the
+// others sets the launch time; with 74 VGPRs the SIMDs of a CU took 6/6/4/4 of its 20 waves
+// (+12 % on C3 against the same code at 88 VGPRs, tools/gpu_ab.sh, r02 log).
+#ifndef ARX_TRACE_WAVES
+#define ARX_TRACE_WAVES 5
+#endif
+#if ARX_TRACE_WAVES == 5
+#define ARX_TRACE_VGPR_FENCE "v87"
+#elif ARX_TRACE_WAVES == 4
+#define ARX_TRACE_VGPR_FENCE "v103"
+#elif ARX_TRACE_WAVES == 6
+#define ARX_TRACE_VGPR_FENCE "v79"
+#else
+#error "ARX_TRACE_WAVES must be 4, 5 or 6"
+#endif
+
 // The persistent trace kernel.  Each wave owns the static ray range [w_next, w_end) of its
 // launch.  Outer loop: shade the lanes whose query finished, refill retired lanes with new rays
 // (directions from the pre-pass), set up the next query of every lane that needs one.  Inner
@@ -467,6 +485,10 @@ __device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav
 template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, bool Q16, bool GSTACK>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     __shared__ int stk_lds[GSTACK ? 1 : kLdsStack * BLOCK];
+    // Hold the VGPR allocation at the count that fits exactly MINW waves per SIMD (see
+    // ARX_TRACE_VGPR_FENCE): the kernel needs ~74, which would let the dispatcher put 6 waves on
+    // some SIMDs and 4 on others.
+    asm volatile("" ::: ARX_TRACE_VGPR_FENCE);
     const int lane = threadIdx.x;
     const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
     using Stack = typename std::conditional<GSTACK, GlobalStack, LdsStack<BLOCK, kLdsStack>>::type;
@@ -576,6 +598,12 @@ __global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __
     R[k] = r;
 }
 
+// dst += src over n int64 bins (a group's shards summed on one device, arx_group.cpp).
+__global__ void hist_add_kernel(long long* __restrict__ dst, const long long* __restrict__ src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
 // Direction pre-pass: float4(dir, 0) for rays [first, first + count).
 __global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -593,25 +621,38 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
     out[3 * i + 2] = d.z;
 }
 
-// Production tuning: 128-lane blocks, 5 waves per SIMD (96 VGPRs,
-// 14.3 KB of LDS stack per block), shade at 12 idle lanes, leaves at 12 pending, 12 node steps
-// per inner iteration.
-constexpr int kThresh = 12, kLeafThresh = 12, kMinWaves = 5, kSteps = 12;
+// Production tuning: 128-lane blocks, exactly kWaves waves per SIMD, shade at
+// 12 idle lanes, leaves at 12 pending, 12 node steps per inner iteration.  The ARX_TRACE_* macros
+// exist only for design experiments (build.py --exp builds a separate library under
+// tools/experiments/); the product build never defines them.
+#ifndef ARX_TRACE_THRESH
+#define ARX_TRACE_THRESH 12
+#endif
+#ifndef ARX_TRACE_STEPS
+#define ARX_TRACE_STEPS 12
+#endif
+constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = 12, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
+constexpr int kSimdsPerCu = 4;
 
 template <bool Q16, bool GSTACK>
 hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
-    auto k = trace_kernel<kBlock, kThresh, kLeafThresh, kMinWaves, kSteps, Q16, GSTACK>;
+    auto k = trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, Q16, GSTACK>;
     const uint64_t n_rays = args.ray_end - args.ray_begin;
-    // persistent grid: as many blocks as fit at once, fewer for small launches (one ray per lane)
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+    // persistent grid: exactly kWaves waves per SIMD on every CU, fewer blocks for small launches
+    // (one ray per lane)
+    constexpr int per_cu = kSimdsPerCu * kWaves * 64 / kBlock;
+#ifdef ARX_TRACE_DYN_LDS
+    static const size_t dyn_lds = ARX_TRACE_DYN_LDS;  // design experiments only
+#else
+    static const size_t dyn_lds = 0;
+#endif
     const uint64_t want = (n_rays + kBlock - 1) / kBlock;
     uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
     if (GSTACK) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
     const int grid = (int)std::max<uint64_t>(1, std::min(want, cap));
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)));
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, args);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), dyn_lds, s, args);
     return hipGetLastError();
 }
 
@@ -631,6 +672,12 @@ hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_r
     const int b = 256;
     const int g = (ir_len + b - 1) / b;
     if (g > 0) hipLaunchKernelGGL(finalize_ir_kernel, dim3(g), dim3(b), 0, s, hist, ir_left, ir_right, ir_len, unit, is_mono);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hipStream_t s) {
+    const uint64_t g = (n + 255) / 256;
+    if (g > 0) hipLaunchKernelGGL(hist_add_kernel, dim3((unsigned)g), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 

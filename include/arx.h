@@ -138,6 +138,50 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
 arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right, size_t ir_len);
 int arx_frac_bits(uint64_t n_rays_total);
 
+/* ---- Multi-GPU ray sharding ------------------------------------------------------------------
+ * No reference equivalent: the reference renders on device 0 only (AudioRenderer.cpp:252) and has
+ * no collective (SURVEY.md §2, §8b "set device count", §8e).  A group holds one renderer per GPU;
+ * rank g of G traces the global ray ids [g*N/G, (g+1)*N/G) of the same N = x*y*z ray launch, and
+ * ONE RCCL all-reduce (int64 SUM over xGMI) of the 2*ir_len fixed-point histogram leaves the full
+ * IR on every member -- exact, so the IR is bitwise independent of G.  Convolution then runs on any
+ * member (arx_group_member + arx_convolute_*). */
+typedef struct arx_group arx_group;
+/* One process driving n_devices GPUs: devices[i] (devices NULL = 0..n_devices-1), ncclCommInitAll
+ * (also for n_devices = 1).  cfg->device is ignored.  Listing ONE device several times
+ * oversubscribes it (e.g. to run the sharded path on a single-GPU box): RCCL cannot take a device
+ * twice, so such a group sums its shards on that device instead (the same exact int64 sum). */
+arx_status arx_group_create(const arx_config* cfg, const int32_t* devices, int32_t n_devices, arx_group** out);
+/* One GPU per process (torchrun-style launch): rank 0 calls arx_group_unique_id and shares the
+ * ARX_GROUP_ID_BYTES bytes out of band; every rank then calls arx_group_create_rank with its rank and
+ * cfg->device (ncclCommInitRank).  id may be NULL when n_ranks == 1. */
+#define ARX_GROUP_ID_BYTES 128
+arx_status arx_group_unique_id(uint8_t* id, size_t id_bytes);
+arx_status arx_group_create_rank(const arx_config* cfg, int32_t n_ranks, int32_t rank, const uint8_t* id,
+                                 size_t id_bytes, arx_group** out);
+void arx_group_destroy(arx_group* g);
+int32_t arx_group_members(const arx_group* g); /* renderers in this process */
+int32_t arx_group_ranks(const arx_group* g);   /* G: shards of the launch */
+/* Member i's renderer (owned by the group; NULL if out of range) for convolution / IR access. */
+arx_renderer* arx_group_member(arx_group* g, int32_t i);
+/* The single-renderer setters, applied to every member. */
+arx_status arx_group_set_scene(arx_group* g, const float* tri_vertices, const float* tri_absorption, int64_t n_tris);
+arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_vertices_local, int64_t n_tris);
+arx_status arx_group_set_emitter(arx_group* g, float x, float y, float z);
+arx_status arx_group_set_listener(arx_group* g, float x, float y, float z, float yaw_deg);
+arx_status arx_group_set_thresholds(arx_group* g, float energy, uint32_t max_bounces);
+arx_status arx_group_set_hrtf_absorption_rate(arx_group* g, float rate);
+arx_status arx_group_set_base_power(arx_group* g, float base_power);
+arx_status arx_group_set_mono_output(arx_group* g, int mono);
+arx_status arx_group_set_seed(arx_group* g, uint64_t seed);
+/* render() over the group: clear, trace every local shard, all-reduce, finalize on every member
+ * (async on the members' streams).  render_ms (if not NULL; synchronises) = the longest shard's
+ * trace kernel time. */
+arx_status arx_group_render(arx_group* g, double* render_ms);
+arx_status arx_group_synchronize(arx_group* g);
+arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
+/* Queries / receiver hits / misses summed over this process's members; times = the longest. */
+arx_status arx_group_get_stats(arx_group* g, arx_stats* out);
+
 /* AudioRenderer::convoluteAudioFile (AudioRenderer.h:31; AudioRenderer.cpp:663-750) over
  * convoluteFromAudioBuffer (kernels.cuh:21; kernels.cu:382-438): 1-s blocks zero padded to
  * ir_len, circular convolution with each IR, overlap-added, tail (len mod sr) unprocessed,

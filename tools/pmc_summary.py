@@ -50,6 +50,8 @@ def main():
                     print(f"  {k:34s} / wave-cycles {c[k] / wc:.3f}")
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             print(f"  L2 hit rate                        {c['TCC_HIT_sum'] / (c['TCC_HIT_sum'] + c['TCC_MISS_sum']):.3f}")
+        if "TCP_UTCL1_TRANSLATION_MISS_sum" in c and "TCP_UTCL1_REQUEST_sum" in c:
+            print(f"  UTCL1 translation miss rate        {c['TCP_UTCL1_TRANSLATION_MISS_sum'] / max(1, c['TCP_UTCL1_REQUEST_sum']):.4f}")
         if "TCP_TCC_READ_REQ_sum" in c and "TCP_TCC_READ_REQ_LATENCY_sum" in c:
             print(f"  mean L2 read latency (cycles)      {c['TCP_TCC_READ_REQ_LATENCY_sum'] / c['TCP_TCC_READ_REQ_sum']:.1f}")
 

@@ -1,18 +1,29 @@
 #!/usr/bin/env python3
-"""Render the bench workload a few times (for profilers)."""
+"""Render the C3 bench workload a few times (for profilers and A/B runs).
+
+    python tools/trace_once.py [n_renders]      # library: ARX_LIB (default: the product libarx.so)
+Prints the median trace-kernel time (HIP events) over the renders after the first."""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+# ARX_PKG_ROOT: import the package from another tree (e.g. a build of an older commit, A/B only)
+sys.path.insert(0, os.environ.get("ARX_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local  # noqa: E402
 from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-s = RenderSettings(rays=(100, 100, 100), sample_rate=48000, base_power=3.62, max_bounces=16)
+rays = tuple(int(v) for v in os.environ.get("RAYS", "100,100,100").split(","))
+s = RenderSettings(rays=rays, sample_rate=48000, base_power=3.62, max_bounces=int(os.environ.get("BOUNCES", "16")))
 r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
 r.setEmitterPosInOptix(CONFERENCE_EMITTER)
 r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-for _ in range(n):
-    ms = r.render()
+ms = [r.render() for _ in range(n)]
 st = r.stats()
-print(f"trace {ms:.3f} ms queries {st['queries']} nodes {st['n_nodes']} depth {st['bvh_depth']}", flush=True)
+irl, irr = r.get_ir()
+chk = int(np.frombuffer(irl.tobytes() + irr.tobytes(), np.uint32).astype(np.uint64).sum())
+med = float(np.median(ms[1:] if n > 1 else ms))
+print(f"trace {med:.3f} ms (median of {max(n - 1, 1)}) queries {st['queries']} nodes {st['n_nodes']} "
+      f"depth {st['bvh_depth']} ir_checksum {chk} lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}",
+      flush=True)
