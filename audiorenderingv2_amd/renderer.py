@@ -51,11 +51,15 @@ class AudioRenderer:
     """AudioRenderer(model, ir_length_in_seconds, sample_rate, materials, rays) (AudioRenderer.h:24)."""
 
     def __init__(self, settings: RenderSettings, scene: Scene | None = None,
-                 receiver: tuple[np.ndarray, np.ndarray] | None = None):
+                 receiver: tuple[np.ndarray, np.ndarray] | None = None, _borrowed: C.c_void_p | None = None):
         self.settings = settings
+        self._owned = _borrowed is None
         self._h = C.c_void_p()
-        cfg = settings.to_c()
-        check(lib().arx_create(C.byref(cfg), C.byref(self._h)))
+        if _borrowed is not None:  # a RenderGroup member: the group owns the handle
+            self._h = _borrowed
+        else:
+            cfg = settings.to_c()
+            check(lib().arx_create(C.byref(cfg), C.byref(self._h)))
         self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
         if receiver is not None:
             self.set_receiver_model(*receiver)
@@ -64,9 +68,9 @@ class AudioRenderer:
 
     # -- lifecycle ---------------------------------------------------------------
     def close(self) -> None:
-        if self._h:
+        if self._h and self._owned:
             lib().arx_destroy(self._h)
-            self._h = C.c_void_p()
+        self._h = C.c_void_p()
 
     def __del__(self):
         try:
@@ -243,6 +247,130 @@ class AudioRenderer:
     def convolute_device(self, d_in: int, n_frames: int, d_out_left: int, d_out_right: int) -> None:
         check(lib().arx_convolute_device(self._h, C.c_void_p(d_in), n_frames, C.c_void_p(d_out_left),
                                          C.c_void_p(d_out_right)))
+
+
+class RenderGroup:
+    """Ray-sharded multi-GPU rendering through libarx.so's native RCCL groups (arx_group_*).
+
+    RenderGroup(settings, devices=[0, 1, ...]) drives several GPUs from this process
+    (ncclCommInitAll); RenderGroup.rank(settings, n_ranks, rank, uid) joins a one-GPU-per-process
+    group (ncclCommInitRank) with the id rank 0 got from RenderGroup.unique_id().  render() =
+    every shard traced + one int64 all-reduce + the IR finalised on every member; member(i) is
+    that member's AudioRenderer (convolution, IR access).  The reference has no equivalent (it
+    renders on device 0, AudioRenderer.cpp:252)."""
+
+    def __init__(self, settings: RenderSettings, devices=None, scene: Scene | None = None,
+                 receiver: tuple[np.ndarray, np.ndarray] | None = None, _rank=None):
+        self.settings = settings
+        self._g = C.c_void_p()
+        cfg = settings.to_c()
+        if _rank is not None:
+            n_ranks, rank, uid = _rank
+            check(lib().arx_group_create_rank(C.byref(cfg), int(n_ranks), int(rank), uid, len(uid) if uid else 0,
+                                              C.byref(self._g)))
+        else:
+            devs = list(devices if devices is not None else [settings.device])
+            arr = (C.c_int32 * len(devs))(*devs)
+            check(lib().arx_group_create(C.byref(cfg), arr, len(devs), C.byref(self._g)))
+        self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
+        self.members = [AudioRenderer(settings, _borrowed=C.c_void_p(lib().arx_group_member(self._g, i)))
+                        for i in range(lib().arx_group_members(self._g))]
+        if receiver is not None:
+            self.set_receiver_model(*receiver)
+        if scene is not None:
+            self.set_scene(scene)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().arx_group_unique_id(buf, 128))
+        return buf.raw
+
+    @classmethod
+    def rank(cls, settings: RenderSettings, n_ranks: int, rank: int, uid: bytes | None, **kw) -> "RenderGroup":
+        return cls(settings, _rank=(n_ranks, rank, uid), **kw)
+
+    def close(self) -> None:
+        for m in getattr(self, "members", []):
+            m._h = C.c_void_p()
+        if self._g:
+            lib().arx_group_destroy(self._g)
+            self._g = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._g
+
+    def member(self, i: int = 0) -> AudioRenderer:
+        return self.members[i]
+
+    @property
+    def n_ranks(self) -> int:
+        return int(lib().arx_group_ranks(self._g))
+
+    def set_scene(self, scene: Scene) -> None:
+        self._scene_v = np.ascontiguousarray(scene.tri_v, np.float32)
+        self._scene_a = np.ascontiguousarray(scene.tri_abs, np.float32)
+        check(lib().arx_group_set_scene(self._g, fptr(self._scene_v), fptr(self._scene_a), scene.n_tris))
+
+    def set_receiver_model(self, left: np.ndarray, right: np.ndarray) -> None:
+        for side, t in enumerate((left, right)):
+            t = np.ascontiguousarray(t, np.float32).reshape(-1, 9)
+            check(lib().arx_group_set_receiver_model(self._g, side, fptr(t), t.shape[0]))
+
+    def setEmitterPosInOptix(self, pos) -> None:
+        check(lib().arx_group_set_emitter(self._g, *(float(v) for v in pos)))
+
+    def setSphereCenterInOptix(self, pos, yaw_deg: float = 0.0) -> None:
+        check(lib().arx_group_set_listener(self._g, *(float(v) for v in pos), float(yaw_deg)))
+
+    def setThresholds(self, energy: float, max_bounces: int) -> None:
+        check(lib().arx_group_set_thresholds(self._g, float(energy), int(max_bounces)))
+
+    def set_hrtf_absorption_rate(self, rate: float) -> None:
+        check(lib().arx_group_set_hrtf_absorption_rate(self._g, float(rate)))
+
+    def setBasePower(self, p: float) -> None:
+        check(lib().arx_group_set_base_power(self._g, float(p)))
+
+    def setMonoOutput(self, mono: bool) -> None:
+        check(lib().arx_group_set_mono_output(self._g, 1 if mono else 0))
+
+    def set_seed(self, seed: int) -> None:
+        check(lib().arx_group_set_seed(self._g, int(seed)))
+
+    def render(self, timed: bool = True) -> float:
+        """Trace all shards + all-reduce + finalize; returns the longest shard's trace ms (timed)
+        or 0.0 without synchronising (timed=False)."""
+        ms = C.c_double()
+        check(lib().arx_group_render(self._g, C.byref(ms) if timed else None))
+        return ms.value
+
+    def synchronize(self) -> None:
+        check(lib().arx_group_synchronize(self._g))
+
+    def get_ir(self) -> tuple[np.ndarray, np.ndarray]:
+        L = np.empty(self.ir_length, np.float32)
+        R = np.empty(self.ir_length, np.float32)
+        check(lib().arx_group_copy_ir(self._g, fptr(L), fptr(R), self.ir_length))
+        return L, R
+
+    def stats(self) -> dict:
+        s = ArxStats()
+        check(lib().arx_group_get_stats(self._g, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in ArxStats._fields_}
 
 
 def place_receiver_vertices(local_xyz: np.ndarray, pos, yaw_deg: float) -> np.ndarray:

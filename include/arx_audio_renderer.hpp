@@ -8,8 +8,9 @@
 //     r->render(&ms); r->convoluteAudioFile(samples, bytes, outL, outR, &conv_ms, &proc_ms);
 // Differences (documented in INTEGRATION.md): the scene is passed as flat triangles with
 // material names instead of an OptixModel*, errors throw arx::Error (the reference
-// throws std::runtime_error / exit()s), and setters take effect at the next render
-// without a full reload().
+// throws std::runtime_error / exit()s), setters take effect at the next render
+// without a full reload(), and a device list shards the rays over several GPUs (the
+// renderer always runs through libarx's group API: arx_group_*, RCCL).
 #pragma once
 
 #include <chrono>
@@ -55,8 +56,16 @@ class AudioRenderer {
   public:
     // AudioRenderer(const OptixModel*, unsigned ir_length_in_seconds, int sample_rate,
     //               std::vector<Material>, gdt::vec3f rays_per_dimension)   (AudioRenderer.h:24)
+    // on one GPU (the reference hard-codes device 0, AudioRenderer.cpp:252) ...
     AudioRenderer(const std::vector<Mesh>& model, unsigned ir_length_in_seconds, int sample_rate,
                   const std::vector<Material>& materials, Vec3 rays_per_dimension, int device = 0,
+                  uint64_t seed = 1)
+        : AudioRenderer(model, ir_length_in_seconds, sample_rate, materials, rays_per_dimension,
+                        std::vector<int32_t>{(int32_t)device}, seed) {}
+    // ... or ray-sharded over several GPUs of this process (arx_group_create: RCCL all-reduce of
+    // the IR histogram; render() returns once every GPU holds the full IR).
+    AudioRenderer(const std::vector<Mesh>& model, unsigned ir_length_in_seconds, int sample_rate,
+                  const std::vector<Material>& materials, Vec3 rays_per_dimension, const std::vector<int32_t>& devices,
                   uint64_t seed = 1) {
         arx_config c;
         arx_default_config(&c);
@@ -65,13 +74,13 @@ class AudioRenderer {
         c.rays_z = (int32_t)rays_per_dimension.z;
         c.ir_length_in_seconds = ir_length_in_seconds;
         c.sample_rate = sample_rate;
-        c.device = device;
         c.seed = seed;
-        check(arx_create(&c, &h_));
+        check(arx_group_create(&c, devices.data(), (int32_t)devices.size(), &g_));
+        h_ = arx_group_member(g_, 0);
         ir_length_ = (size_t)ir_length_in_seconds * (size_t)sample_rate;
         setScene(model, materials);
     }
-    ~AudioRenderer() { arx_destroy(h_); }
+    ~AudioRenderer() { arx_group_destroy(g_); }
     AudioRenderer(const AudioRenderer&) = delete;
     AudioRenderer& operator=(const AudioRenderer&) = delete;
 
@@ -92,7 +101,7 @@ class AudioRenderer {
                 ta.push_back(a);
             }
         }
-        check(arx_set_scene(h_, tv.data(), ta.data(), (int64_t)ta.size()));
+        check(arx_group_set_scene(g_, tv.data(), ta.data(), (int64_t)ta.size()));
     }
     // HalfSphere meshes (leftHalf.obj / rightHalf.obj) in their local frame.
     void setReceiverModel(const Mesh& left, const Mesh& right) {
@@ -102,13 +111,16 @@ class AudioRenderer {
             for (size_t t = 0; t + 2 < m[side]->index.size(); t += 3)
                 for (int k = 0; k < 3; ++k)
                     for (int c = 0; c < 3; ++c) tv.push_back(m[side]->vertex[3 * (size_t)m[side]->index[t + k] + c]);
-            check(arx_set_receiver_model(h_, side, tv.data(), (int64_t)(tv.size() / 9)));
+            check(arx_group_set_receiver_model(g_, side, tv.data(), (int64_t)(tv.size() / 9)));
         }
     }
 
-    void render(double* render_time = nullptr) { check(arx_render(h_, render_time)); }  // :27
+    void render(double* render_time = nullptr) {  // :27
+        check(arx_group_render(g_, render_time));
+        if (!render_time) check(arx_group_synchronize(g_));
+    }
 
-    // :31 -- sizes in bytes, host buffers owned by the caller
+    // :31 -- sizes in bytes, host buffers owned by the caller (convolved on the first GPU)
     void convoluteAudioFile(float* h_inputBuffer, size_t h_inputBufferSize, float* h_outputBuffer_left,
                             float* h_outputBuffer_right, double* convolute_time = nullptr,
                             double* convolute_process_time = nullptr) {
@@ -116,13 +128,13 @@ class AudioRenderer {
                                        convolute_time, convolute_process_time));
     }
 
-    void setEmitterPosInOptix(Vec3 p) { check(arx_set_emitter(h_, p.x, p.y, p.z)); }          // :33
+    void setEmitterPosInOptix(Vec3 p) { check(arx_group_set_emitter(g_, p.x, p.y, p.z)); }  // :33
     // placeReceiver(sphere, model, camera, yaw) + setSphereCenterInOptix(camera) in one call
-    void setSphereCenterInOptix(Vec3 p, float yaw_deg = 0.0f) { check(arx_set_listener(h_, p.x, p.y, p.z, yaw_deg)); }
-    void setThresholds(float energy, unsigned int max_bounces) { check(arx_set_thresholds(h_, energy, max_bounces)); }
-    void set_hrtf_absorption_rate(float v) { check(arx_set_hrtf_absorption_rate(h_, v)); }
-    void setBasePower(float v) { check(arx_set_base_power(h_, v)); }
-    void setMonoOutput(bool v) { check(arx_set_mono_output(h_, v ? 1 : 0)); }
+    void setSphereCenterInOptix(Vec3 p, float yaw_deg = 0.0f) { check(arx_group_set_listener(g_, p.x, p.y, p.z, yaw_deg)); }
+    void setThresholds(float energy, unsigned int max_bounces) { check(arx_group_set_thresholds(g_, energy, max_bounces)); }
+    void set_hrtf_absorption_rate(float v) { check(arx_group_set_hrtf_absorption_rate(g_, v)); }
+    void setBasePower(float v) { check(arx_group_set_base_power(g_, v)); }
+    void setMonoOutput(bool v) { check(arx_group_set_mono_output(g_, v ? 1 : 0)); }
     // :47 -- declared by the reference, body empty (AudioRenderer.cpp:574-576); kept for source
     // compatibility, it does nothing (the live path zips L/R in pass_d_live)
     void normalizeAndMergeStereoOutput(double*, double*, size_t, double*) {}
@@ -170,17 +182,20 @@ class AudioRenderer {
         write_output_ = false;
     }
 
-    void getIR(float* left, float* right) { check(arx_copy_ir(h_, left, right, ir_length_)); }
+    void getIR(float* left, float* right) { check(arx_group_copy_ir(g_, left, right, ir_length_)); }
     arx_stats stats() {
         arx_stats s;
-        check(arx_get_stats(h_, &s));
+        check(arx_group_get_stats(g_, &s));
         return s;
     }
     size_t irLength() const { return ir_length_; }
-    arx_renderer* handle() { return h_; }
+    int gpuCount() const { return arx_group_ranks(g_); }
+    arx_renderer* handle() { return h_; }  // the first GPU's renderer
+    arx_group* group() { return g_; }
 
   private:
-    arx_renderer* h_ = nullptr;
+    arx_group* g_ = nullptr;
+    arx_renderer* h_ = nullptr;  // member 0, owned by g_
     size_t ir_length_ = 0;
     std::vector<double> live_scratch_;
     bool write_ir_ = false, write_output_ = false, experimentation_ = false;
