@@ -115,6 +115,13 @@ SIGNATURES = {
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
+    "arx_trace_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "arx_stream_create": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
+    "arx_stream_destroy": (None, [_P]),
+    "arx_stream_reset": (C.c_int, [_P]),
+    "arx_stream_info": (C.c_int, [_P, _I32, _I32, _I32]),
+    "arx_stream_process": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
+    "arx_stream_process_device": (C.c_int, [_P, C.c_void_p, C.c_size_t, C.c_void_p]),
     "arx_group_create": (C.c_int, [C.POINTER(ArxConfig), _I32, C.c_int32, C.POINTER(_P)]),
     "arx_group_unique_id": (C.c_int, [C.c_char_p, C.c_size_t]),
     "arx_group_create_rank": (C.c_int, [C.POINTER(ArxConfig), C.c_int32, C.c_int32, C.c_char_p, C.c_size_t,

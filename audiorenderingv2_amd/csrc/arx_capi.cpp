@@ -223,7 +223,33 @@ arx_status ensure_device_scene(arx_renderer* r) {
 
 }  // namespace
 
+arx_status arx::last_trace_ms(arx_renderer* r, bool wait, double* ms) {
+    if (r->trace_launches == 0) return fail(ARX_ERR_NOT_READY, "no trace launch yet");
+    const int slot = (int)((r->trace_launches - 1) % arx_renderer::kTraceRing);
+    if (wait) ARX_HIP(hipEventSynchronize(r->tev1[slot]));
+    float f = 0.f;
+    ARX_HIP(hipEventElapsedTime(&f, r->tev0[slot], r->tev1[slot]));
+    *ms = f;
+    return ARX_OK;
+}
+
 extern "C" {
+
+arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
+    if (!r || (n > 0 && !ms)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    const uint64_t have = std::min<uint64_t>(r->trace_launches, (uint64_t)arx_renderer::kTraceRing);
+    const uint64_t k = std::min<uint64_t>(have, (uint64_t)n);
+    for (uint64_t i = 0; i < k; ++i) {  // oldest of the last k first
+        const int slot = (int)((r->trace_launches - k + i) % arx_renderer::kTraceRing);
+        ARX_HIP(hipEventSynchronize(r->tev1[slot]));
+        float f = 0.f;
+        ARX_HIP(hipEventElapsedTime(&f, r->tev0[slot], r->tev1[slot]));
+        ms[i] = f;
+    }
+    if (n_out) *n_out = (size_t)k;
+    return ARX_OK;
+}
 
 const char* arx_status_string(arx_status s) {
     switch (s) {
@@ -296,13 +322,17 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     };
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&r->ev0)) != hipSuccess || (e = hipEventCreate(&r->ev1)) != hipSuccess ||
+        (e = hipEventCreate(&r->cev0)) != hipSuccess || (e = hipEventCreate(&r->cev1)) != hipSuccess ||
+        (e = hipEventCreate(&r->lev0)) != hipSuccess || (e = hipEventCreate(&r->lev1)) != hipSuccess ||
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&r->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
+    for (int i = 0; i < arx_renderer::kTraceRing; ++i)
+        if ((e = hipEventCreate(&r->tev0[i])) != hipSuccess || (e = hipEventCreate(&r->tev1[i])) != hipSuccess)
+            return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
@@ -331,8 +361,12 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_conv_in);
     hipFree(r->d_conv_out);
     if (r->h_counters) hipHostFree(r->h_counters);
-    if (r->ev0) hipEventDestroy(r->ev0);
-    if (r->ev1) hipEventDestroy(r->ev1);
+    for (int i = 0; i < arx_renderer::kTraceRing; ++i) {
+        if (r->tev0[i]) hipEventDestroy(r->tev0[i]);
+        if (r->tev1[i]) hipEventDestroy(r->tev1[i]);
+    }
+    for (hipEvent_t ev : {r->cev0, r->cev1, r->lev0, r->lev1})
+        if (ev) hipEventDestroy(ev);
     if (r->own_stream) hipStreamDestroy(r->own_stream);
     delete r;
 }
@@ -506,9 +540,11 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         a.gstack = r->d_gstack;
         a.gstack_lanes = lanes;
     }
-    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
+    ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
-    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
+    ++r->trace_launches;
     return ARX_OK;
 }
 
@@ -521,6 +557,7 @@ arx_status arx_finalize_ir(arx_renderer* r) {
                                r->cfg.is_mono, r->stream));
     r->conv_ir_dirty = true;
     r->conv_live_ir_dirty = true;
+    ++r->ir_generation;
     return ARX_OK;
 }
 
@@ -531,12 +568,7 @@ arx_status arx_render(arx_renderer* r, double* render_ms) {
     if (st != ARX_OK) return st;
     st = arx_finalize_ir(r);
     if (st != ARX_OK) return st;
-    if (render_ms) {
-        ARX_HIP(hipEventSynchronize(r->ev1));
-        float ms = 0.f;
-        ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
-        *render_ms = ms;
-    }
+    if (render_ms) return last_trace_ms(r, true, render_ms);
     return ARX_OK;
 }
 
@@ -583,8 +615,10 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     r->stats.queries = r->h_counters[0];
     r->stats.receiver_hits = r->h_counters[1];
     r->stats.misses = r->h_counters[2];
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, r->ev0, r->ev1) == hipSuccess) r->stats.trace_ms = ms;
+    double tms = 0.0;
+    if (last_trace_ms(r, false, &tms) == ARX_OK) r->stats.trace_ms = tms;
+    float cms = 0.f;
+    if (r->conv_launches > 0 && hipEventElapsedTime(&cms, r->cev0, r->cev1) == hipSuccess) r->stats.conv_ms = cms;
     *out = r->stats;
     return ARX_OK;
 }
@@ -608,6 +642,7 @@ arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right
     ARX_HIP(hipStreamSynchronize(r->stream));
     r->conv_ir_dirty = true;
     r->conv_live_ir_dirty = true;
+    ++r->ir_generation;
     return ARX_OK;
 }
 
@@ -658,9 +693,10 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     ARX_HIP(hipSetDevice(r->cfg.device));
     arx_status st = ensure_conv(r);
     if (st != ARX_OK) return st;
-    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    ARX_HIP(hipEventRecord(r->cev0, r->stream));
     ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, r->stream));
-    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    ARX_HIP(hipEventRecord(r->cev1, r->stream));
+    ++r->conv_launches;
     return ARX_OK;
 }
 
@@ -694,7 +730,7 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
     ARX_HIP(hipEventSynchronize(p1));
     float ms = 0.f;
     if (conv_ms) {
-        ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
+        ARX_HIP(hipEventElapsedTime(&ms, r->cev0, r->cev1));
         *conv_ms = ms;
     }
     if (proc_ms) {
@@ -714,9 +750,9 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
     ARX_HIP(hipSetDevice(r->cfg.device));
     arx_status st = ensure_conv_live(r, (int32_t)std::max<size_t>(n_in, 1));
     if (st != ARX_OK) return st;
-    ARX_HIP(hipEventRecord(r->ev0, r->stream));
+    ARX_HIP(hipEventRecord(r->lev0, r->stream));
     ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
-    ARX_HIP(hipEventRecord(r->ev1, r->stream));
+    ARX_HIP(hipEventRecord(r->lev1, r->stream));
     return ARX_OK;
 }
 
@@ -759,6 +795,102 @@ arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first, uint64_t coun
     if (e == hipSuccess) e = hipMemcpy(h_out, d, 3 * count * sizeof(float), hipMemcpyDeviceToHost);
     hipFree(d);
     if (e != hipSuccess) return fail(ARX_ERR_HIP, "ray directions: %s", hipGetErrorString(e));
+    return ARX_OK;
+}
+
+// ---- streaming convolution (UPOLS, arx_conv.hip) --------------------------------------------------
+}  // extern "C"
+
+struct arx_stream {
+    arx_renderer* r = nullptr;
+    StreamPlan* plan = nullptr;
+    uint64_t ir_generation = ~0ull;  // the IR the partition spectra were made from
+    double* d_in = nullptr;          // host-API staging: block frames in, 2 * block out
+    double* d_out = nullptr;
+};
+
+extern "C" {
+
+arx_status arx_stream_create(arx_renderer* r, int32_t block_frames, arx_stream** out) {
+    if (!r || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out = nullptr;
+    if (block_frames <= 0 || block_frames > 4096 || block_frames > r->ir_len)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "stream block of %d frames: must be in [1, min(4096, ir_len)]", block_frames);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_stream* s = new (std::nothrow) arx_stream();
+    if (!s) return fail(ARX_ERR_OUT_OF_MEMORY, "host allocation failed");
+    s->r = r;
+    char err[256] = {0};
+    s->plan = stream_plan_create(r->ir_len, block_frames, r->cfg.device, err, sizeof(err));
+    if (!s->plan) {
+        delete s;
+        return fail(ARX_ERR_INTERNAL, "stream plan: %s", err);
+    }
+    if (hipMalloc(&s->d_in, (size_t)block_frames * sizeof(double)) != hipSuccess ||
+        hipMalloc(&s->d_out, 2 * (size_t)block_frames * sizeof(double)) != hipSuccess) {
+        arx_stream_destroy(s);
+        return fail(ARX_ERR_OUT_OF_MEMORY, "stream buffers");
+    }
+    *out = s;
+    return ARX_OK;
+}
+
+void arx_stream_destroy(arx_stream* s) {
+    if (!s) return;
+    hipSetDevice(s->r->cfg.device);
+    hipStreamSynchronize(s->r->stream);
+    stream_plan_destroy(s->plan);
+    hipFree(s->d_in);
+    hipFree(s->d_out);
+    delete s;
+}
+
+arx_status arx_stream_reset(arx_stream* s) {
+    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    ARX_HIP(hipSetDevice(s->r->cfg.device));
+    ARX_HIP(stream_reset(s->plan, s->r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_stream_info(const arx_stream* s, int32_t* block, int32_t* partitions, int32_t* fft_size) {
+    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    if (block) *block = stream_plan_block(s->plan);
+    if (partitions) *partitions = stream_plan_partitions(s->plan);
+    if (fft_size) *fft_size = stream_plan_fft(s->plan);
+    return ARX_OK;
+}
+
+arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n_frames, double* d_out) {
+    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    const int32_t B = stream_plan_block(s->plan);
+    if (n_frames > (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "%zu frames exceed the stream block %d", n_frames, B);
+    if ((n_frames > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    arx_renderer* r = s->r;
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (s->ir_generation != r->ir_generation) {  // the IR changed: new partition spectra
+        ARX_HIP(stream_set_ir(s->plan, r->d_ir, r->d_ir + r->ir_len, r->stream));
+        s->ir_generation = r->ir_generation;
+    }
+    ARX_HIP(hipEventRecord(r->lev0, r->stream));
+    ARX_HIP(stream_run(s->plan, d_in, (int64_t)n_frames, d_out, r->stream));
+    ARX_HIP(hipEventRecord(r->lev1, r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames, double* h_out, size_t out_len) {
+    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    const int32_t B = stream_plan_block(s->plan);
+    if (out_len != 2 * (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "output must hold 2*block = %d doubles", 2 * B);
+    if (n_frames > (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "%zu frames exceed the stream block %d", n_frames, B);
+    if ((n_frames > 0 && !h_in) || !h_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    arx_renderer* r = s->r;
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (n_frames > 0)
+        ARX_HIP(hipMemcpyAsync(s->d_in, h_in, n_frames * sizeof(double), hipMemcpyHostToDevice, r->stream));
+    const arx_status st = arx_stream_process_device(s, s->d_in, n_frames, s->d_out);
+    if (st != ARX_OK) return st;
+    ARX_HIP(hipMemcpyAsync(h_out, s->d_out, out_len * sizeof(double), hipMemcpyDeviceToHost, r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));
     return ARX_OK;
 }
 

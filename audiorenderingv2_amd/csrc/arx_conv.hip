@@ -560,17 +560,12 @@ void conv_plan_destroy(ConvPlan* p) {
 
 const char* conv_plan_describe(const ConvPlan* p) { return p ? p->desc : ""; }
 
-// Pass B: the wave-per-row pass (pass_bw) for rows of 512 or 256; ARX_CONV_B512=0 takes the
-// generic radix-4 pass (design A/B).
+// Pass B: the wave-per-row pass (pass_bw) for rows of 512 or 256, else the generic radix-4 pass.
 template <int MODE>
 static void launch_pass_b(const ConvPlan* p, unsigned batches, const PassArgs& a, hipStream_t s) {
-    static const bool on = [] {
-        const char* e = std::getenv("ARX_CONV_B512");
-        return !(e && e[0] == '0');
-    }();
-    if (on && p->N2 == 512 && p->N1 % 4 == 0)
+    if (p->N2 == 512 && p->N1 % 4 == 0)
         hipLaunchKernelGGL((pass_bw<MODE, 512>), dim3(p->N1 / 4, batches), dim3(kThreads), (4 + 1) * 512 * sizeof(double2), s, a);
-    else if (on && p->N2 == 256 && p->N1 % 4 == 0)
+    else if (p->N2 == 256 && p->N1 % 4 == 0)
         hipLaunchKernelGGL((pass_bw<MODE, 256>), dim3(p->N1 / 4, batches), dim3(kThreads), (4 + 1) * 256 * sizeof(double2), s, a);
     else
         hipLaunchKernelGGL(pass_b<MODE>, dim3(p->N1, batches), dim3(kThreads), 2 * (size_t)p->N2 * sizeof(double2), s, a);
@@ -594,6 +589,7 @@ static PassArgs base_args(const ConvPlan* p) {
 }
 
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
+    (void)hipGetLastError();  // report this launch's error, not a stale one
     PassArgs a = base_args(p);
     a.ir_l = d_ir_left;
     a.ir_r = d_ir_right;
@@ -626,6 +622,7 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
         if (e != hipSuccess) return e;
         p->pairs_cap = pairs;
     }
+    (void)hipGetLastError();  // report this launch's error, not a stale one
     PassArgs a = base_args(p);
     a.in = d_in;
     a.S = p->d_S;
@@ -660,6 +657,7 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
         if (e != hipSuccess) return e;
         p->pairs_cap = 1;
     }
+    (void)hipGetLastError();  // report this launch's error, not a stale one
     PassArgs a = base_args(p);
     a.in_d = d_in;
     a.n_in = n_in;
@@ -676,5 +674,186 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     hipLaunchKernelGGL(pass_d_live, dim3((unsigned)((p->n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
+
+// ==================================================================================================
+// Streaming convolution for the RtAudio duplex callback: uniformly
+// partitioned overlap-save (UPOLS) in f64, replacing the reference's per-callback full-length
+// circular convolution (AudioRenderer.cpp:593-661, kernels.cu:345-377) whose 2*ir_len outputs the
+// CircularBuffer then wraps onto itself (main.cpp:189-195).  Per block of B frames:
+//   fwd  X_b = FFT_N(last N input samples)                   (one workgroup, LDS, N <= 8192)
+//   mac  Z   = sum_p X_(b-p) * G_p,  G_p = FFT_N(hL_p + i hR_p), h_p = h[pB, (p+1)B) zero padded
+//   inv  y_L + i y_R = IFFT_N(Z)[N-B, N)                     (one workgroup, LDS)
+// N = the power of two >= 2B, P = ceil(ir_len / B).  Because h_L and h_R are real, one complex
+// spectrum per partition (G_p) and one inverse FFT serve both ears.  Output: B frames zipped L/R,
+// scaled like the reference's live path, ir_len / (ir_len/2) x the linear convolution
+// (normalizeBuffers, kernels.cu:450-467), but without the circular wrap and the CircularBuffer
+// aliasing.  The frequency-domain delay line keeps input spectra, so a new IR (a moving listener)
+// takes effect at the next block without a glitch-inducing restart.
+struct StreamPlan {
+    int32_t B = 0, N = 0, lgN = 0, P = 0, n = 0;
+    int64_t blocks = 0;           // processed since reset (slot of block b = b % P)
+    double2* d_tw = nullptr;      // W_N^e
+    double2* d_G = nullptr;       // P * N partition spectra
+    double2* d_X = nullptr;       // P * N input spectra ring (frequency-domain delay line)
+    double2* d_Z = nullptr;       // N accumulated spectrum
+    double* d_hist = nullptr;     // N - B input history
+    double scale = 0.0;
+};
+
+namespace {
+
+constexpr int kStreamThreads = 1024;  // lds_fft needs >= N/16 threads
+
+// G_p = FFT_N(hL[pB + i] + i hR[pB + i], i < B, zero padded): one workgroup per partition.
+__global__ __launch_bounds__(kStreamThreads) void stream_ir_kernel(const float* __restrict__ hl,
+                                                                   const float* __restrict__ hr, int32_t n,
+                                                                   int32_t B, int32_t N, int32_t lgN,
+                                                                   const double2* __restrict__ tw,
+                                                                   double2* __restrict__ G) {
+    extern __shared__ double2 buf[];
+    const int p = blockIdx.x;
+    for (int i = threadIdx.x; i < N; i += kStreamThreads) {
+        const int64_t k = (int64_t)p * B + i;
+        buf[i] = (i < B && k < n) ? make_double2((double)hl[k], (double)hr[k]) : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    lds_fft(buf, N, lgN, -1, threadIdx.x, kStreamThreads, tw, N);
+    for (int i = threadIdx.x; i < N; i += kStreamThreads) G[(size_t)p * N + i] = buf[i];
+}
+
+// X_b = FFT_N([history (N - B), block (B)]), history <- the window's last N - B samples.
+__global__ __launch_bounds__(kStreamThreads) void stream_fwd_kernel(const double* __restrict__ in, int32_t n_in,
+                                                                    double* __restrict__ hist, int32_t B, int32_t N,
+                                                                    int32_t lgN, const double2* __restrict__ tw,
+                                                                    double2* __restrict__ X) {
+    extern __shared__ double2 buf[];
+    const int H = N - B;
+    for (int i = threadIdx.x; i < N; i += kStreamThreads) {
+        double v;
+        if (i < H) v = hist[i];
+        else v = (i - H < n_in) ? in[i - H] : 0.0;
+        buf[i] = make_double2(v, 0.0);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < H; i += kStreamThreads) hist[i] = buf[i + B].x;
+    lds_fft(buf, N, lgN, -1, threadIdx.x, kStreamThreads, tw, N);  // (its first barrier orders the reads above)
+    for (int i = threadIdx.x; i < N; i += kStreamThreads) X[i] = buf[i];
+}
+
+// Z[k] = sum_p X_((b - p) mod P)[k] * G_p[k]: one thread per bin, coalesced over k.
+__global__ __launch_bounds__(256) void stream_mac_kernel(const double2* __restrict__ X, const double2* __restrict__ G,
+                                                         int32_t P, int32_t N, int32_t newest,
+                                                         double2* __restrict__ Z) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= N) return;
+    double2 acc = make_double2(0.0, 0.0);
+    int slot = newest;
+    for (int p = 0; p < P; ++p) {
+        const double2 x = X[(size_t)slot * N + k];
+        const double2 g = G[(size_t)p * N + k];
+        acc.x = fma(x.x, g.x, fma(-x.y, g.y, acc.x));
+        acc.y = fma(x.x, g.y, fma(x.y, g.x, acc.y));
+        slot = slot == 0 ? P - 1 : slot - 1;
+    }
+    Z[k] = acc;
+}
+
+// y_L + i y_R = IFFT_N(Z)[N - B, N), zipped and scaled.
+__global__ __launch_bounds__(kStreamThreads) void stream_inv_kernel(const double2* __restrict__ Z, int32_t B,
+                                                                    int32_t N, int32_t lgN,
+                                                                    const double2* __restrict__ tw, double scale,
+                                                                    double* __restrict__ out) {
+    extern __shared__ double2 buf[];
+    for (int i = threadIdx.x; i < N; i += kStreamThreads) buf[i] = Z[i];
+    __syncthreads();
+    lds_fft(buf, N, lgN, +1, threadIdx.x, kStreamThreads, tw, N);
+    for (int i = threadIdx.x; i < B; i += kStreamThreads) {
+        const double2 v = buf[N - B + i];
+        out[2 * i] = v.x * scale;
+        out[2 * i + 1] = v.y * scale;
+    }
+}
+
+}  // namespace
+
+StreamPlan* stream_plan_create(int32_t ir_len, int32_t block, int device, char* err, size_t errlen) {
+    auto bad = [&](const char* m) -> StreamPlan* {
+        if (err && errlen) std::snprintf(err, errlen, "%s", m);
+        return nullptr;
+    };
+    if (ir_len <= 0 || block <= 0 || block > 4096) return bad("stream block must be in [1, 4096] frames");
+    StreamPlan* p = new StreamPlan();
+    p->B = block;
+    p->lgN = ilog2(2 * (int64_t)block);
+    p->lgN = std::max(p->lgN, 4);
+    p->N = 1 << p->lgN;
+    p->P = (int32_t)(((int64_t)ir_len + block - 1) / block);
+    p->n = ir_len;
+    p->scale = (double)ir_len / ((double)p->N * (double)(ir_len / 2));  // unnormalised IFFT, / (ir_len/2)
+    hipSetDevice(device);
+    std::vector<double2> tw((size_t)p->N);
+    const long double two_pi = 6.283185307179586476925286766559L;
+    for (int64_t e = 0; e < p->N; ++e) {
+        const long double ang = two_pi * (long double)e / (long double)p->N;
+        tw[(size_t)e] = make_double2((double)cosl(ang), -(double)sinl(ang));
+    }
+    const size_t spec = (size_t)p->P * p->N * sizeof(double2);
+    if (hipMalloc(&p->d_tw, (size_t)p->N * sizeof(double2)) != hipSuccess || hipMalloc(&p->d_G, spec) != hipSuccess ||
+        hipMalloc(&p->d_X, spec) != hipSuccess || hipMalloc(&p->d_Z, (size_t)p->N * sizeof(double2)) != hipSuccess ||
+        hipMalloc(&p->d_hist, (size_t)(p->N - p->B + 1) * sizeof(double)) != hipSuccess ||
+        hipMemcpy(p->d_tw, tw.data(), (size_t)p->N * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(p->d_G, 0, spec) != hipSuccess) {
+        stream_plan_destroy(p);
+        return bad("device allocation failed");
+    }
+    if (stream_reset(p, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        stream_plan_destroy(p);
+        return bad("stream reset failed");
+    }
+    return p;
+}
+
+void stream_plan_destroy(StreamPlan* p) {
+    if (!p) return;
+    hipFree(p->d_tw);
+    hipFree(p->d_G);
+    hipFree(p->d_X);
+    hipFree(p->d_Z);
+    hipFree(p->d_hist);
+    delete p;
+}
+
+hipError_t stream_reset(StreamPlan* p, hipStream_t s) {
+    p->blocks = 0;
+    hipError_t e = hipMemsetAsync(p->d_X, 0, (size_t)p->P * p->N * sizeof(double2), s);
+    if (e == hipSuccess) e = hipMemsetAsync(p->d_hist, 0, (size_t)(p->N - p->B + 1) * sizeof(double), s);
+    return e;
+}
+
+hipError_t stream_set_ir(StreamPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
+    (void)hipGetLastError();  // report this launch's error, not a stale one
+    hipLaunchKernelGGL(stream_ir_kernel, dim3(p->P), dim3(kStreamThreads), (size_t)p->N * sizeof(double2), s, d_ir_left,
+                       d_ir_right, p->n, p->B, p->N, p->lgN, p->d_tw, p->d_G);
+    return hipGetLastError();
+}
+
+hipError_t stream_run(StreamPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s) {
+    (void)hipGetLastError();  // report this launch's error, not a stale one
+    if (n_in < 0 || n_in > p->B) return hipErrorInvalidValue;
+    const int32_t slot = (int32_t)(p->blocks % p->P);
+    const size_t lds = (size_t)p->N * sizeof(double2);
+    hipLaunchKernelGGL(stream_fwd_kernel, dim3(1), dim3(kStreamThreads), lds, s, d_in, (int32_t)n_in, p->d_hist, p->B,
+                       p->N, p->lgN, p->d_tw, p->d_X + (size_t)slot * p->N);
+    hipLaunchKernelGGL(stream_mac_kernel, dim3((unsigned)((p->N + 255) / 256)), dim3(256), 0, s, p->d_X, p->d_G, p->P,
+                       p->N, slot, p->d_Z);
+    hipLaunchKernelGGL(stream_inv_kernel, dim3(1), dim3(kStreamThreads), lds, s, p->d_Z, p->B, p->N, p->lgN, p->d_tw,
+                       p->scale, d_out_interleaved);
+    ++p->blocks;
+    return hipGetLastError();
+}
+
+int32_t stream_plan_block(const StreamPlan* p) { return p ? p->B : 0; }
+int32_t stream_plan_partitions(const StreamPlan* p) { return p ? p->P : 0; }
+int32_t stream_plan_fft(const StreamPlan* p) { return p ? p->N : 0; }
 
 }  // namespace arx

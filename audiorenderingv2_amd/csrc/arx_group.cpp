@@ -271,10 +271,10 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         double worst = 0.0;
         for (arx_renderer* r : g->members) {
             ARX_HIP(hipSetDevice(r->cfg.device));
-            ARX_HIP(hipEventSynchronize(r->ev1));
-            float ms = 0.f;
-            ARX_HIP(hipEventElapsedTime(&ms, r->ev0, r->ev1));
-            worst = std::max(worst, (double)ms);
+            double ms = 0.0;
+            const arx_status st = last_trace_ms(r, true, &ms);
+            if (st != ARX_OK) return st;
+            worst = std::max(worst, ms);
         }
         *render_ms = worst;
     }

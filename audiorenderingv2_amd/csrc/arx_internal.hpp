@@ -34,6 +34,12 @@ inline uint64_t n_rays(const arx_config& c) {
 
 }  // namespace arx
 
+struct arx_renderer;
+namespace arx {
+// Device time (ms) of the renderer's last trace launch; wait = synchronise on it first.
+arx_status last_trace_ms(arx_renderer* r, bool wait, double* ms);
+}  // namespace arx
+
 // One renderer = one device (AudioRenderer, AudioRenderer.h:16-152).
 struct arx_renderer {
     arx_config cfg;
@@ -41,7 +47,14 @@ struct arx_renderer {
     int cus = 256;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // timing events: a ring of (start, end) pairs around the last kTraceRing trace launches
+    // (arx_trace_times), and separate pairs for the file and the live convolution
+    static constexpr int kTraceRing = 64;
+    hipEvent_t tev0[kTraceRing] = {}, tev1[kTraceRing] = {};
+    uint64_t trace_launches = 0;
+    hipEvent_t cev0 = nullptr, cev1 = nullptr;  // file convolution
+    uint64_t conv_launches = 0;
+    hipEvent_t lev0 = nullptr, lev1 = nullptr;  // live convolution
 
     float emitter[3] = {0.f, 0.f, 0.f};
     float center[3] = {0.f, 0.f, 0.f};
@@ -79,6 +92,7 @@ struct arx_renderer {
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;  // pinned
 
+    uint64_t ir_generation = 0;  // bumped whenever the IR changes (finalize_ir, set_ir): streams re-transform
     arx::ConvPlan* conv_live = nullptr;  // mic path plan (block = live block length)
     bool conv_live_ir_dirty = true;
     double* d_live_in = nullptr;

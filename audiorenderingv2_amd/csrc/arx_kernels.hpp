@@ -38,4 +38,17 @@ const char* conv_plan_describe(const ConvPlan* p);
 hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s);
 int32_t conv_plan_block(const ConvPlan* p);
 
+// ---- streaming convolution (arx_conv.hip): uniformly partitioned overlap-save, f64 ----
+struct StreamPlan;  // opaque
+// block: frames per callback (<= 4096); FFT size = the power of two >= 2*block.
+StreamPlan* stream_plan_create(int32_t ir_len, int32_t block, int device, char* err, size_t errlen);
+void stream_plan_destroy(StreamPlan* p);
+hipError_t stream_reset(StreamPlan* p, hipStream_t s);                      // zero history + delay line
+hipError_t stream_set_ir(StreamPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s);
+// One block (n_in <= block f64 frames, zero padded) -> 2*block zipped L/R doubles.
+hipError_t stream_run(StreamPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s);
+int32_t stream_plan_block(const StreamPlan* p);
+int32_t stream_plan_partitions(const StreamPlan* p);
+int32_t stream_plan_fft(const StreamPlan* p);
+
 }  // namespace arx

@@ -466,6 +466,9 @@ __device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav
 #ifndef ARX_TRACE_WAVES
 #define ARX_TRACE_WAVES 5
 #endif
+#ifndef ARX_TRACE_COUNT
+#define ARX_TRACE_COUNT 0  // 1: count node steps / leaf triangle tests into counters[4..5]
+#endif
 #if ARX_TRACE_WAVES == 5
 #define ARX_TRACE_VGPR_FENCE "v87"
 #elif ARX_TRACE_WAVES == 4
@@ -507,6 +510,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     uint64_t w_next = n * wave_id / n_waves;
     const uint64_t w_end = n * (wave_id + 1) / n_waves;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
+#if ARX_TRACE_COUNT  // measurement builds only (build.py --exp ... -D ARX_TRACE_COUNT=1)
+    uint32_t n_steps = 0, n_tris = 0;
+#endif
     bool active = false, trav = false, exhausted = w_next >= w_end;
     RayState s;
     s.depth = -1;
@@ -574,13 +580,25 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
 #pragma unroll
                 for (int k = 0; k < NSTEPS; ++k)
-                    if (t.node >= 0) node_step<Q16>(r, oix, oiy, oiz, t, stk, nrs);
+                    if (t.node >= 0) {
+#if ARX_TRACE_COUNT
+                        ++n_steps;
+#endif
+                        node_step<Q16>(r, oix, oiy, oiz, t, stk, nrs);
+                    }
             } else if (t.node <= -2) {
+#if ARX_TRACE_COUNT
+                n_tris += (uint32_t)((~t.node) & 15);
+#endif
                 leaf_step(a, r, t, stk);
             }
         }
     }
     flush_counters(a, n_q, n_rx, n_miss, lane);
+#if ARX_TRACE_COUNT  // [4] node steps, [5] leaf triangle tests (lane level)
+    atomicAdd(a.counters + 4, (unsigned long long)n_steps);
+    atomicAdd(a.counters + 5, (unsigned long long)n_tris);
+#endif
 }
 
 __global__ void finalize_ir_kernel(const long long* __restrict__ hist, float* __restrict__ L, float* __restrict__ R,
@@ -660,6 +678,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
 
 hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_global_stack) {
     if (a.ray_end <= a.ray_begin) return hipSuccess;
+    (void)hipGetLastError();  // report this launch's error, not a stale one of an earlier runtime call
     if (!a.dirs || !a.cnodes || !a.tris || !a.hist || !a.counters) return hipErrorInvalidValue;
     const bool gstack = force_global_stack || a.bvh_depth + 1 > kLdsStack;
     if (gstack && (!a.gstack || a.gstack_lanes < (uint64_t)kBlock)) return hipErrorInvalidValue;
@@ -669,6 +688,7 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_g
 
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len, double unit,
                               int32_t is_mono, hipStream_t s) {
+    (void)hipGetLastError();
     const int b = 256;
     const int g = (ir_len + b - 1) / b;
     if (g > 0) hipLaunchKernelGGL(finalize_ir_kernel, dim3(g), dim3(b), 0, s, hist, ir_left, ir_right, ir_len, unit, is_mono);
@@ -676,12 +696,14 @@ hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_r
 }
 
 hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hipStream_t s) {
+    (void)hipGetLastError();
     const uint64_t g = (n + 255) / 256;
     if (g > 0) hipLaunchKernelGGL(hist_add_kernel, dim3((unsigned)g), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s) {
+    (void)hipGetLastError();
     const int b = 256;
     const uint64_t g = (count + b - 1) / b;
     if (g > 0) hipLaunchKernelGGL(ray_dir_kernel, dim3((unsigned)g), dim3(b), 0, s, seed, first, count, d_out);

@@ -206,6 +206,13 @@ class AudioRenderer:
         R = np.ascontiguousarray(right, np.float32)
         check(lib().arx_set_ir(self._h, fptr(L), fptr(R), L.size))
 
+    def trace_times(self, n: int = 64) -> np.ndarray:
+        """Device ms of the last min(n, 64) trace launches, oldest first (arx_trace_times)."""
+        out = np.zeros(n, np.float64)
+        k = C.c_size_t()
+        check(lib().arx_trace_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
+        return out[:k.value]
+
     def stats(self) -> dict:
         s = ArxStats()
         check(lib().arx_get_stats(self._h, C.byref(s)))
@@ -247,6 +254,47 @@ class AudioRenderer:
     def convolute_device(self, d_in: int, n_frames: int, d_out_left: int, d_out_right: int) -> None:
         check(lib().arx_convolute_device(self._h, C.c_void_p(d_in), n_frames, C.c_void_p(d_out_left),
                                          C.c_void_p(d_out_right)))
+
+
+class LiveStream:
+    """Streaming convolution of a renderer's IR (arx_stream_*, uniformly partitioned overlap-save
+    in f64): process(block) consumes one block of <= block_frames f64 frames and returns
+    block_frames output frames zipped L/R -- the linear convolution of the input stream with the
+    current IR at the reference live path's scale (ir_len / (ir_len/2)).  The drop-in successor of
+    convoluteLiveInput + CircularBuffer (AudioRenderer.cpp:593-661, main.cpp:99-135), whose
+    full-length circular result the reference's buffer wraps onto itself."""
+
+    def __init__(self, renderer: AudioRenderer, block_frames: int = 4096):
+        self.renderer = renderer
+        self._s = C.c_void_p()
+        check(lib().arx_stream_create(renderer.handle, int(block_frames), C.byref(self._s)))
+        b, p, n = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().arx_stream_info(self._s, C.byref(b), C.byref(p), C.byref(n)))
+        self.block_frames, self.partitions, self.fft_size = b.value, p.value, n.value
+
+    def process(self, block: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(block, np.float64)
+        out = np.empty(2 * self.block_frames, np.float64)
+        D = C.POINTER(C.c_double)
+        check(lib().arx_stream_process(self._s, x.ctypes.data_as(D), x.size, out.ctypes.data_as(D), out.size))
+        return out
+
+    def process_device(self, d_in: int, n_frames: int, d_out: int) -> None:
+        check(lib().arx_stream_process_device(self._s, C.c_void_p(d_in), int(n_frames), C.c_void_p(d_out)))
+
+    def reset(self) -> None:
+        check(lib().arx_stream_reset(self._s))
+
+    def close(self) -> None:
+        if self._s:
+            lib().arx_stream_destroy(self._s)
+            self._s = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RenderGroup:

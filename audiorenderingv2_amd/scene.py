@@ -84,6 +84,24 @@ def test_obj_scene(materials=()) -> Scene:
     return scene_from_meshes(load_meshes_npz(os.path.join(GOLDEN, "test_obj.npz")), materials)
 
 
+REFERENCE_AUDIO = {
+    "guitar": "audio_guitar_16k_ch0.npz",           # R/guitar_sample_16k.wav (C1)
+    "experimento": "audio_experimento_16k_ch0.npz",  # R/experimento_entrada_16KHz.wav (C2)
+    "clapper": "audio_clapper_48k_ch0.npz",          # R/assets/sound_samples/A_Clapper_Board.wav (C3)
+}
+
+
+def reference_audio(name: str) -> tuple[np.ndarray, int]:
+    """Channel 0 of a reference WAV as the reference's AudioFile decodes it (golden fixture made by
+    tests/golden/make_golden.py through oracle/_ref/refdump): (f32 samples, sample rate)."""
+    d = np.load(os.path.join(GOLDEN, REFERENCE_AUDIO[name]))
+    if "pcm16" in d:
+        x = d["pcm16"].astype(np.float32) / np.float32(32768.0)
+    else:
+        x = d["f32"].astype(np.float32)
+    return x, int(d["sample_rate"])
+
+
 def reference_config_materials() -> list:
     """pathtracer_parameters.materials of R/config.json (parsed by the reference's cJSON)."""
     with open(os.path.join(GOLDEN, "config_parsed.json")) as fh:

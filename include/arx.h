@@ -132,6 +132,10 @@ arx_status arx_finalize_ir(arx_renderer* r);
 arx_status arx_ir_device(arx_renderer* r, float** d_left, float** d_right, size_t* ir_len);
 arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir_len);
 arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
+/* Device times (HIP events on the renderer's stream) of the last min(n, 64) trace launches, oldest
+ * first, into ms[0..*n_out); synchronises on them.  The reference's timed window (Time taken by
+ * Optix, AudioRenderer.cpp:495-518), kept per launch so a benchmark can average a timed region. */
+arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 /* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */
@@ -206,6 +210,25 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
  * next convolution: which = 1 file path, 2 live path, 3 both.  Lets a moving-listener frame
  * (re-trace + reduce + new spectra) finish before audio needs it. */
 arx_status arx_prepare_ir_spectra(arx_renderer* r, int which);
+
+/* Streaming convolution for the RtAudio duplex callback (replaces the
+ * per-callback full-length circular convolution of convoluteLiveInput, AudioRenderer.cpp:593-661,
+ * whose 2*ir_len outputs the reference's CircularBuffer wraps onto itself, main.cpp:189-195, which
+ * stays available as arx_convolute_live_block -- the compat path).  Uniformly partitioned
+ * overlap-save in f64 on the renderer's device and stream: each call consumes one block of
+ * n_frames <= block_frames f64 input frames (shorter blocks are zero padded) and returns
+ * block_frames output frames zipped L/R (2*block_frames doubles) = the linear convolution of the
+ * input stream with the renderer's current IR, scaled like the reference's live path
+ * (ir_len / (ir_len/2), normalizeBuffers).  Latency: one block.  A new IR (render, set_ir) applies
+ * from the next block on; the input history is kept.  block_frames in [1, min(4096, ir_len)]. */
+typedef struct arx_stream arx_stream;
+arx_status arx_stream_create(arx_renderer* r, int32_t block_frames, arx_stream** out);
+void arx_stream_destroy(arx_stream* s);
+arx_status arx_stream_reset(arx_stream* s); /* forget the input history */
+arx_status arx_stream_info(const arx_stream* s, int32_t* block_frames, int32_t* partitions, int32_t* fft_size);
+arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames, double* h_out, size_t out_len);
+/* Same on device buffers (n_frames f64 in, 2*block_frames f64 out), no host synchronisation. */
+arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n_frames, double* d_out);
 
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,

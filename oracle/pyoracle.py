@@ -42,6 +42,11 @@ class OrcRayRecord(C.Structure):
 _lib = None
 
 
+class OrcStream(C.Structure):
+    _fields_ = [("block", C.c_int32), ("N", C.c_int32), ("P", C.c_int32), ("ir_len", C.c_int32),
+                ("blocks", C.c_int64), ("hist", C.c_void_p), ("X", C.c_void_p), ("G", C.c_void_p)]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
@@ -76,6 +81,11 @@ def lib() -> C.CDLL:
         L.orc_fft.restype = C.c_int
         L.orc_convolute_live_block.argtypes = [C.POINTER(C.c_double), C.c_int64, F, F, C.c_int32,
                                                C.POINTER(C.c_double)]
+        L.orc_stream_init.argtypes = [C.POINTER(OrcStream), C.c_int32, F, F, C.c_int32]
+        L.orc_stream_init.restype = C.c_int
+        L.orc_stream_process.argtypes = [C.POINTER(OrcStream), C.POINTER(C.c_double), C.c_int64,
+                                         C.POINTER(C.c_double)]
+        L.orc_stream_free.argtypes = [C.POINTER(OrcStream)]
         _lib = L
     return _lib
 
@@ -199,3 +209,28 @@ def convolute_live_block(x: np.ndarray, ir_left: np.ndarray, ir_right: np.ndarra
                                    _f(np.ascontiguousarray(ir_right, np.float32)), n,
                                    out.ctypes.data_as(C.POINTER(C.c_double)))
     return out
+
+
+class Stream:
+    """orc_stream_*: the streaming convolution (uniformly partitioned overlap-save) restated."""
+
+    def __init__(self, block: int, ir_left: np.ndarray, ir_right: np.ndarray):
+        self._s = OrcStream()
+        self._l = np.ascontiguousarray(ir_left, np.float32)
+        self._r = np.ascontiguousarray(ir_right, np.float32)
+        if lib().orc_stream_init(C.byref(self._s), int(block), _f(self._l), _f(self._r), self._l.size) != 0:
+            raise RuntimeError("orc_stream_init failed")
+        self.block = int(block)
+
+    def process(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.zeros(2 * self.block, np.float64)
+        lib().orc_stream_process(C.byref(self._s), x.ctypes.data_as(C.POINTER(C.c_double)), x.size,
+                                 out.ctypes.data_as(C.POINTER(C.c_double)))
+        return out
+
+    def __del__(self):
+        try:
+            lib().orc_stream_free(C.byref(self._s))
+        except Exception:
+            pass

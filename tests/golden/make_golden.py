@@ -79,7 +79,32 @@ def wav_fixture(path: str) -> dict:
     }
 
 
+def audio_fixture(path: str, out: str) -> None:
+    """Channel 0 of a reference WAV as the reference's AudioFile decoded it, for the GPU tests and
+    bench.py (the reference tree is absent on the GPU box).  16-bit PCM is stored as its integer
+    codes (AudioFile: sample = code / 32768, AudioFile.h:1242-1245), IEEE float as float32."""
+    lines = refdump("wav", path)
+    sr, ch, n, bits = (int(x) for x in lines[0].split()[1:])
+    x = np.array([float.fromhex(v) for v in lines[1:1 + n]], dtype=np.float32)
+    if bits == 16:
+        codes = np.rint(x.astype(np.float64) * 32768.0).astype(np.int16)
+        assert np.array_equal((codes.astype(np.float32) / np.float32(32768.0)), x)
+        np.savez_compressed(out, sample_rate=sr, bit_depth=bits, channels=ch, pcm16=codes)
+    else:
+        np.savez_compressed(out, sample_rate=sr, bit_depth=bits, channels=ch, f32=x)
+
+
+def audio_fixtures() -> None:
+    audio_fixture(os.path.join(REF, "guitar_sample_16k.wav"), os.path.join(HERE, "audio_guitar_16k_ch0.npz"))
+    audio_fixture(os.path.join(REF, "experimento_entrada_16KHz.wav"), os.path.join(HERE, "audio_experimento_16k_ch0.npz"))
+    audio_fixture(os.path.join(REF, "assets", "sound_samples", "A_Clapper_Board.wav"),
+                  os.path.join(HERE, "audio_clapper_48k_ch0.npz"))
+
+
 def main() -> int:
+    if len(sys.argv) > 1 and sys.argv[1] == "audio":
+        audio_fixtures()
+        return 0
     if not os.path.exists(REFDUMP):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     left = os.path.join(MODELS, "leftHalf.obj")
@@ -98,6 +123,7 @@ def main() -> int:
             wav_fixture(os.path.join(REF, "assets", "sound_samples", "A_Clapper_Board.wav"))]
     with open(os.path.join(HERE, "wav_decode.json"), "w") as fh:
         json.dump(wavs, fh)
+    audio_fixtures()
     cfg = {}
     mats = []
     for line in refdump("config", os.path.join(REF, "config.json")):

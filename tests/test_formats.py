@@ -95,6 +95,24 @@ def test_wav_matches_golden():
             assert float(np.sum(w.samples[c].astype(np.float64) ** 2)) == fx["sumsq"][c]
 
 
+def test_reference_audio_fixtures_match_golden():
+    """The full channel-0 fixtures (tests/golden/audio_*.npz, used by GPU tests and bench.py where
+    the reference tree is absent) agree with the independent head / strided / sum records of the
+    reference's AudioFile decode (wav_decode.json)."""
+    from audiorenderingv2_amd.scene import reference_audio
+
+    with open(os.path.join(GOLDEN, "wav_decode.json")) as fh:
+        fixtures = {os.path.basename(fx["file"]): fx for fx in json.load(fh)}
+    for name, fname in (("guitar", "guitar_sample_16k.wav"), ("experimento", "experimento_entrada_16KHz.wav"),
+                        ("clapper", "A_Clapper_Board.wav")):
+        x, sr = reference_audio(name)
+        fx = fixtures[fname]
+        assert sr == fx["sample_rate"] and x.size == fx["samples_per_channel"]
+        np.testing.assert_array_equal(bits(x[:256]), bits(np.array(fx["head"][0], np.float32)))
+        np.testing.assert_array_equal(bits(x[::997]), bits(np.array(fx["strided_997"][0], np.float32)))
+        assert float(np.sum(x, dtype=np.float64)) == fx["sum"][0]
+
+
 def config_as_fixture(c):
     d = {
         "initial_volume": c.initial_volume, "ir_length_in_seconds": c.ir_length_in_seconds, "width": c.width,

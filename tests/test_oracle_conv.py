@@ -101,3 +101,56 @@ def test_live_block_matches_numpy():
     for ch, ir in enumerate((irl, irr)):
         ref = np.fft.ifft(np.fft.fft(seg) * np.fft.fft(ir.astype(np.float64))).real * n / (n // 2)
         np.testing.assert_allclose(got[ch::2], ref, rtol=1e-10, atol=1e-10)
+
+
+# ---- streaming convolution (uniformly partitioned overlap-save, orc_stream_*) -------------------
+def stream_all(block, hl, hr, x, cuts=None):
+    st = po.Stream(block, hl, hr)
+    outs, pos = [], 0
+    for n in cuts or [block] * (-(-x.size // block)):
+        outs.append(st.process(x[pos:pos + n]))
+        pos += n
+    return np.concatenate(outs)
+
+
+@pytest.mark.parametrize("ir_len,block", [(1000, 64), (1000, 100), (441, 441), (3000, 4096 // 8), (88200, 4096)])
+def test_stream_oracle_equals_linear_convolution(ir_len, block):
+    rng = np.random.default_rng(ir_len + block)
+    hl = rng.standard_normal(ir_len).astype(np.float32)
+    hr = (rng.standard_normal(ir_len) * (rng.random(ir_len) < 0.05)).astype(np.float32)
+    nb = 6 if ir_len > 50000 else 25
+    x = rng.uniform(-1, 1, block * nb)
+    out = stream_all(block, hl, hr, x)
+    scale = ir_len / (ir_len // 2)
+    for ch, h in ((0, hl), (1, hr)):
+        ref = np.convolve(x, h.astype(np.float64))[:x.size] * scale
+        assert np.abs(out[ch::2] - ref).max() <= 1e-13 * np.abs(ref).max()
+
+
+def test_stream_oracle_short_blocks_are_zero_padded():
+    rng = np.random.default_rng(2)
+    hl, hr = rng.standard_normal(500).astype(np.float32), rng.standard_normal(500).astype(np.float32)
+    cuts = [64, 10, 64, 0, 37, 64]
+    x = rng.uniform(-1, 1, sum(cuts))
+    out = stream_all(64, hl, hr, x, cuts)
+    padded = np.concatenate([np.pad(x[sum(cuts[:i]):sum(cuts[:i + 1])], (0, 64 - c)) for i, c in enumerate(cuts)])
+    ref = np.convolve(padded, hl.astype(np.float64))[:padded.size] * (500 / 250)
+    assert np.abs(out[0::2] - ref).max() <= 1e-13 * np.abs(ref).max()
+
+
+def test_stream_equals_compat_path_when_tails_do_not_wrap():
+    """The reference's live path (per block: full-length circular convolution, accumulated at
+    the block's offset) equals the stream when the IR support leaves room for a block
+    (support <= ir_len - block) and the accumulator does not wrap."""
+    rng = np.random.default_rng(4)
+    n, block, nb = 4000, 256, 12
+    hl = np.zeros(n, np.float32)
+    hr = np.zeros(n, np.float32)
+    hl[:n - block] = rng.standard_normal(n - block)
+    hr[rng.integers(0, n - block, 40)] = 1.0
+    x = rng.uniform(-1, 1, block * nb)
+    acc = np.zeros(2 * (block * nb + n))
+    for b in range(nb):
+        acc[2 * b * block:2 * b * block + 2 * n] += po.convolute_live_block(x[b * block:(b + 1) * block], hl, hr)
+    out = stream_all(block, hl, hr, x)
+    assert np.abs(out - acc[:out.size]).max() <= 1e-12 * np.abs(acc).max()

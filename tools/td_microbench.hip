@@ -58,6 +58,14 @@ __global__ void gather(const float4* __restrict__ table, uint32_t n_blocks, int 
 }
 
 int main() {
+    {  // device limits the trace kernel's launch geometry depends on
+        int v[4] = {0, 0, 0, 0};
+        hipDeviceGetAttribute(&v[0], hipDeviceAttributeMaxSharedMemoryPerBlock, 0);
+        hipDeviceGetAttribute(&v[1], hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, 0);
+        hipDeviceGetAttribute(&v[2], hipDeviceAttributeSharedMemPerBlockOptin, 0);
+        hipDeviceGetAttribute(&v[3], hipDeviceAttributeClockRate, 0);
+        std::printf("lds per block %d, per CU %d, opt-in per block %d, clock %d kHz\n", v[0], v[1], v[2], v[3]);
+    }
     const size_t bytes = 16u << 20;
     const uint32_t n_blocks = (uint32_t)(bytes / 64);
     float4* table;
@@ -95,7 +103,9 @@ int main() {
         ms /= reps;
         const double instr_per_cu = (double)waves_per_cu * ITERS;
         const double cyc = ms * 1e-3 * 2.1e9;  // ~effective clock under load
-        std::printf("%-40s %.3f ms  %.1f cycles per wave-instruction per CU\n", c.name, ms, cyc / instr_per_cu);
+        const double lane_loads = (double)grid * block * ITERS * ((c.mode == 3) ? (double)c.active / 64.0 : 1.0);
+        std::printf("%-40s %.3f ms  %.1f cycles per wave-instruction per CU  %.4g 16-B lane loads/s\n", c.name, ms,
+                    cyc / instr_per_cu, lane_loads / (ms * 1e-3));
     }
     return 0;
 }

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Node steps and leaf triangle tests per closest-hit query of the C3 trace launch, from a
+counting build of the library (build.py --exp count -D ARX_TRACE_COUNT=1; counters[4..5]).
+Feeds the vector-memory (TD) roofline of DESIGN.md section 6: a node step is two 16-B lane
+loads (QNode2), a triangle test three (TriRec), shading three more and the direction one.
+
+    ARX_LIB=tools/experiments/lib/libarx_count.so python tools/trace_counts.py
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local  # noqa: E402
+from audiorenderingv2_amd._lib import check, lib  # noqa: E402
+from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  # noqa: E402
+
+s = RenderSettings(rays=(100, 100, 100), sample_rate=48000, base_power=3.62, max_bounces=16)
+r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
+r.setEmitterPosInOptix(CONFERENCE_EMITTER)
+r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+ms = r.render()
+c = (C.c_uint64 * 8)()
+check(lib().arx_debug_trace_counters(r.handle, c, 8))
+q, steps, tris = c[0], c[4], c[5]
+loads = 2 * steps + 3 * tris + 3 * q + 1 * 10**6
+print(json.dumps({"workload": "c3", "queries": q, "node_steps": steps, "tri_tests": tris,
+                  "steps_per_query": steps / q, "tri_tests_per_query": tris / q,
+                  "lane_loads_16B_per_query": loads / q, "trace_ms_counting_build": ms}))
