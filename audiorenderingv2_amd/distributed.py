@@ -1,11 +1,17 @@
-"""Ray-sharded multi-GPU rendering: one process per GPU, torch.distributed over RCCL.
+"""Process-group helpers for ray-sharded multi-GPU runs (one process per GPU).
 
-The reference is single-GPU (device 0 hard-coded, AudioRenderer.cpp:252).  Here rank r
-of W traces the global ray ids [r*N/W, (r+1)*N/W) of the same launch (the Philox key
-is the global id, so the union of shards is exactly the single-GPU launch) into an
-int64 fixed-point histogram, and ONE all-reduce (SUM, int64) over xGMI combines the
-2*ir_len bins -- exact, so the IR is bitwise independent of W.  That all-reduce is the
-path's only exchange step.
+The product's multi-GPU path is native: libarx's groups (arx_group_*, RenderGroup) shard the
+rays and all-reduce the int64 IR histogram with RCCL themselves.  torch.distributed is only an
+optional caller-side convenience: the bootstrap of a one-process-per-GPU group (broadcasting
+rank 0's RCCL unique id), barriers and max-over-ranks timing in bench.py, and an alternative
+histogram all-reduce (allreduce_histogram) for callers that keep the histogram in a torch tensor
+(arx_attach_histogram).
+
+The reference is single-GPU (device 0 hard-coded, AudioRenderer.cpp:252).  Rank r of W traces
+the global ray ids [r*N/W, (r+1)*N/W) of the same launch (the Philox key is the global id, so
+the union of shards is exactly the single-GPU launch) into an int64 fixed-point histogram, and
+ONE all-reduce (SUM, int64) over xGMI combines the 2*ir_len bins -- exact, so the IR is bitwise
+independent of W.  That all-reduce is the path's only exchange step.
 """
 from __future__ import annotations
 
@@ -47,6 +53,13 @@ def allreduce_histogram(hist: torch.Tensor) -> torch.Tensor:
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(hist, op=dist.ReduceOp.SUM)
     return hist
+
+
+def broadcast_object(objs: list, src: int = 0) -> list:
+    """In-place broadcast of a list of picklable objects from rank src (e.g. the RCCL unique id)."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast_object_list(objs, src=src)
+    return objs
 
 
 def barrier() -> None:

@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """Headline benchmark: ray-bounces/s (+ convolved audio frames/s) on the conference scene.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 One step = one pass of the hot path on every rank (BASELINE.json configs[2], per GPU):
-  clear the int64 IR histogram -> trace this rank's 1M-ray shard x 16 bounces (fused HIP
-  kernel) -> RCCL all-reduce (SUM int64) of the 2 x 96000-bin histogram -> finalize the
-  stereo f32 IR -> IR spectra + file-mode FFT convolution of 807498 frames (48 kHz).
+  trace this rank's 1M-ray shard x 16 bounces (fused HIP kernel) -> one RCCL all-reduce (int64
+  SUM) of the 2 x 96000-bin histogram -> finalize the stereo f32 IR (libarx's native group API,
+  arx_group_render) -> IR spectra + file-mode FFT convolution of A_Clapper_Board.wav channel 0
+  (807 498 frames, 48 kHz).
+The group is native: a one-GPU RCCL communicator (ncclCommInitAll) for N = 1, one
+ncclCommInitRank rank per process under torchrun (the RCCL unique id is shared once through
+torch.distributed, which otherwise only carries the barrier and the max-over-ranks timing).
 Inputs are resident in HBM before timing.  Rank 0 prints ONE JSON line.
-Scaling is weak: every rank owns 1M rays of a W*1M-ray launch (energy normalised by the
-total count, devicePrograms.cu:208) and convolves its own 807498-frame stream.
+Scaling is weak: every rank owns 1M rays of a W*1M-ray launch (energy normalised by the total
+count, devicePrograms.cu:208) and convolves its own copy of the stream.
 """
 from __future__ import annotations
 
@@ -31,17 +35,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
     # configs[2]: conference, 1M rays x 16 bounces, 48 kHz IR + convolution (per GPU)
-    "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, frames=807498,
+    "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, audio="clapper",
                desc="configs[2]: conference stand-in, 1M rays x 16 bounces per GPU, 48 kHz IR (96000 bins/ear), "
-                    "file-mode FFT convolution of 807498 frames (A_Clapper_Board length) per GPU"),
+                    "file-mode FFT convolution of A_Clapper_Board.wav ch0 (807498 frames) per GPU"),
     # configs[1]: conference, 100K rays x 8 bounces, 16 kHz
-    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, frames=128000,
+    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento",
                desc="configs[1]: conference stand-in, 100K rays x 8 bounces per GPU, 16 kHz IR, "
-                    "convolution of 128000 frames (experimento_entrada_16KHz length) per GPU"),
+                    "convolution of experimento_entrada_16KHz.wav (128000 frames) per GPU"),
     # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the ranks (strong)
-    "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, frames=807498, total=True,
+    "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, audio="clapper", total=True,
                desc="configs[3]: conference stand-in, 10M rays x 32 bounces in total, ray-sharded across the "
-                    "ranks, 48 kHz IR, RCCL IR all-reduce; convolution of 807498 frames per GPU"),
+                    "ranks, 48 kHz IR, RCCL IR all-reduce; convolution of A_Clapper_Board.wav ch0 per GPU"),
 }
 
 
@@ -53,15 +57,9 @@ def bytes_per_bounce(n_tris: int) -> int:
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
 
 
-def synthetic_audio(frames: int, sr: int, seed: int = 0) -> np.ndarray:
-    rng = np.random.default_rng(seed)
-    t = np.arange(frames) / sr
-    x = 0.5 * np.sin(2 * np.pi * 440.0 * t) * np.exp(-3.0 * (t % 1.0)) + 0.05 * rng.standard_normal(frames)
-    return x.astype(np.float32)
-
-
-def cpu_baseline(scene, receiver, wl, n_total_rays, budget_s: float) -> dict:
-    """The CPU oracle (naive C ray loop + simple BVH) on this host's cores, bounded sample."""
+def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> dict:
+    """The CPU oracle (naive C ray loop + median-split BVH) on this host, bounded samples of the
+    same launch: one thread, and every core this process may run on (sched_getaffinity)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as po
     from audiorenderingv2_amd.renderer import place_receiver_vertices
@@ -75,29 +73,35 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, budget_s: float) -> dict:
     osc = po.Scene(tv, ta, bvh=True)
     p = po.make_params(rays=(n_total_rays, 1, 1), sample_rate=wl["sample_rate"], base_power=3.62,
                        max_bounces=wl["max_bounces"], emitter=CONFERENCE_EMITTER, listener=CONFERENCE_LISTENER)
-    threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
-    n = 4000
-    t0 = time.perf_counter()
-    _, _, st = osc.trace(p, 0, n, threads=threads)
-    dt = time.perf_counter() - t0
-    rate_rays = n / max(dt, 1e-6)
-    n2 = int(min(max(rate_rays * budget_s, n), 4_000_000))
-    t0 = time.perf_counter()
-    _, _, st = osc.trace(p, 0, n2, threads=threads)
-    dt = time.perf_counter() - t0
-    # convolution leg: f64 oracle FFT block convolution of a bounded slice
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+    def timed(threads: int, seconds: float) -> tuple[float, int, float]:
+        n = 500 * threads
+        t0 = time.perf_counter()
+        osc.trace(p, 0, n, threads=threads)
+        rate = n / max(time.perf_counter() - t0, 1e-6)
+        n2 = int(min(max(rate * seconds, n), 4_000_000))
+        t0 = time.perf_counter()
+        _, _, st = osc.trace(p, 0, n2, threads=threads)
+        dt = time.perf_counter() - t0
+        return st["queries"] / dt, n2, dt
+
+    one, n1, d1 = timed(1, budget_s / 2)
+    allc, n2, d2 = timed(cores, budget_s / 2)
+    # convolution leg: the f64 oracle block convolution of a bounded slice of the same audio
     sr = wl["sample_rate"]
     ir = np.zeros(2 * sr, np.float32)
     ir[::97] = 1e-4
-    x = synthetic_audio(min(wl["frames"], 8 * sr), sr)
+    x = audio[:min(audio.size, 8 * sr)]
     t1 = time.perf_counter()
     po.convolute_audio(x, sr, ir)
     po.convolute_audio(x, sr, ir)
     dtc = time.perf_counter() - t1
     return {
-        "value": st["queries"] / dt, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
-        "sample": f"oracle/arx_oracle.c (-O3, median-split BVH, {threads} pthreads): rays 0..{n2} of the same "
-                  f"launch ({st['queries']} closest-hit queries, {dt:.1f} s)",
+        "value": allc, "unit": "ray-bounces/s", "cores": cores, "kind": "port",
+        "sample": f"oracle/arx_oracle.c (-O3, median-split BVH): rays 0..{n2} of the same launch on {cores} "
+                  f"threads ({d2:.1f} s); 1 thread: rays 0..{n1} ({d1:.1f} s)",
+        "single_thread_value": one,
         "convolved_frames_per_s": x.size / (dtc / 2),
         "convolution_sample": f"f64 oracle block convolution, 1 thread, {x.size} frames x 2 ears",
         "cpu_model": _cpu_model(),
@@ -115,41 +119,97 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def moving_listener(r, D, dev, stream, hist, ray_begin, ray_end, frames: int) -> dict:
+def moving_listener(g, D, dev, frames: int, rays_per_rank: int) -> dict:
     """the listener moves 0.05 m/frame along +x with yaw += 1 deg/frame.
-    Frame latency = host wall time of: receiver re-placement (host transform + sub-tree BVH
-    rebuild + upload, no scene rebuild) -> clear -> trace this rank's shard -> RCCL all-reduce
-    -> finalize IR -> new IR spectra for the file and live convolution paths, synchronised.
-    The reference instead re-places the receiver and rebuilds the whole GAS and pipeline
-    (OptixModel.cpp:153-257, AudioRenderer.cpp:466-486, 790-798).  p50/p99 are max over ranks."""
-    import torch
-
+    Frame latency = host wall time of: receiver re-placement (receiver sub-tree only, no scene
+    rebuild) -> trace this rank's shard -> RCCL all-reduce -> finalize IR -> new IR spectra for
+    the file and the live convolution paths, synchronised.  The reference instead re-places the
+    receiver and rebuilds the whole GAS and pipeline (OptixModel.cpp:153-257,
+    AudioRenderer.cpp:466-486, 790-798).  p50/p99 are max over ranks."""
     from audiorenderingv2_amd.scene import CONFERENCE_LISTENER
 
     x0, y0, z0 = CONFERENCE_LISTENER
+    m = g.member(0)
     lat = []
     for k in range(frames + 3):
-        torch.cuda.synchronize(dev)
+        g.synchronize()
         t0 = time.perf_counter()
-        r.setSphereCenterInOptix((x0 + 0.05 * k, y0, z0), float(k % 360))
-        r.clear_histogram()
-        r.trace_rays(ray_begin, ray_end)
-        D.allreduce_histogram(hist)
-        r.finalize_ir()
-        r.prepare_ir_spectra(file=True, live=True)
-        stream.synchronize()
+        g.setSphereCenterInOptix((x0 + 0.05 * k, y0, z0), float(k % 360))
+        g.render(timed=False)
+        m.prepare_ir_spectra(file=True, live=True)
+        g.synchronize()
         if k >= 3:  # first frames warm the receiver rebuild path
             lat.append((time.perf_counter() - t0) * 1e3)
     a = np.array(lat)
-    p50 = D.max_over_ranks(float(np.percentile(a, 50)), dev)
-    p99 = D.max_over_ranks(float(np.percentile(a, 99)), dev)
-    return {"frames": frames, "p50_ms": p50, "p99_ms": p99, "max_ms": D.max_over_ranks(float(a.max()), dev),
-            "budget_ms": 1000.0 / 60.0,
+    return {"frames": frames, "rays_per_rank": rays_per_rank, "p50_ms": D.max_over_ranks(float(np.percentile(a, 50)), dev),
+            "p99_ms": D.max_over_ranks(float(np.percentile(a, 99)), dev),
+            "max_ms": D.max_over_ranks(float(a.max()), dev), "budget_ms": 1000.0 / 60.0,
             "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + all-reduce + finalize + IR spectra"}
 
 
-def load_traffic() -> dict | None:
-    path = os.path.join(REPO, "profiles", "trace_traffic.json")
+def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: int) -> dict:
+    """C5's per-rank frame on 8 GPUs: 1M rays per frame split 8 ways is 125K rays per rank.  One
+    renderer traces rays [0, shard) of the 1M launch per frame (plus re-placement, finalize and
+    IR spectra); the 8-GPU all-reduce of 768 kB adds ~10-20 us over xGMI."""
+    from audiorenderingv2_amd import AudioRenderer
+    from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER
+
+    r = AudioRenderer(settings, scene=scene, receiver=receiver)
+    r.setEmitterPosInOptix(CONFERENCE_EMITTER)
+    x0, y0, z0 = CONFERENCE_LISTENER
+    lat = []
+    for k in range(frames + 3):
+        t0 = time.perf_counter()
+        r.setSphereCenterInOptix((x0 + 0.05 * k, y0, z0), float(k % 360))
+        r.clear_histogram()
+        r.trace_rays(0, shard)
+        r.finalize_ir()
+        r.prepare_ir_spectra(file=True, live=True)
+        r.stats()  # synchronises the renderer's stream
+        if k >= 3:
+            lat.append((time.perf_counter() - t0) * 1e3)
+    r.close()
+    a = np.array(lat)
+    return {"frames": frames, "rays_per_rank": shard, "p50_ms": float(np.percentile(a, 50)),
+            "p99_ms": float(np.percentile(a, 99)), "max_ms": float(a.max()), "budget_ms": 1000.0 / 60.0,
+            "per_frame": "one rank's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra "
+                         "(projected 8-GPU rank; the all-reduce is not included)"}
+
+
+def streaming_leg(r, audio, block: int, dev) -> dict:
+    """C3's streaming overlap-add leg: the same audio fed through the streaming convolution
+    (arx_stream_*: uniformly partitioned overlap-save, f64) in 4096-frame blocks, device-resident
+    (arx_stream_process_device): per-block device latency and frames/s."""
+    import torch
+
+    from audiorenderingv2_amd import LiveStream
+
+    s = LiveStream(r, block)
+    x = torch.from_numpy(audio.astype(np.float64)).to(dev)
+    nb = audio.size // block
+    out = torch.empty(2 * block, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for b in range(8):  # warm-up
+        s.process_device(x[b * block:].data_ptr(), block, out.data_ptr())
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(nb + 1)]
+    torch.cuda.synchronize(dev)
+    ev[0].record(stream)
+    for b in range(nb):
+        s.process_device(x[b * block:].data_ptr(), block, out.data_ptr())
+        ev[b + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    per = np.array([ev[b].elapsed_time(ev[b + 1]) for b in range(nb)])
+    total_ms = ev[0].elapsed_time(ev[nb])
+    s.close()
+    return {"block_frames": block, "blocks": nb, "partitions": s.partitions, "fft_size": s.fft_size,
+            "frames_per_s": nb * block / (total_ms * 1e-3), "block_p50_ms": float(np.percentile(per, 50)),
+            "block_p99_ms": float(np.percentile(per, 99)),
+            "block_period_ms": 1e3 * block / 48000.0,
+            "method": "device-resident, back-to-back blocks on the renderer stream, HIP events per block"}
+
+
+def load_profile(name: str) -> dict | None:
+    path = os.path.join(REPO, "profiles", name)
     if os.path.exists(path):
         with open(path) as fh:
             return json.load(fh)
@@ -162,17 +222,18 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
+    ap.add_argument("--no-streaming", action="store_true")
     args = ap.parse_args(argv)
 
     import torch
 
-    from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local
+    from audiorenderingv2_amd import RenderGroup, RenderSettings, conference_standin, receiver_local
     from audiorenderingv2_amd import distributed as D
-    from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER
+    from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, reference_audio
 
     rank, world, local = D.init()
     if not torch.cuda.is_available():
@@ -183,55 +244,52 @@ def main(argv=None) -> int:
     rx, ry, rz = wl["rays"]
     if wl.get("total"):  # a fixed total split over the ranks (strong scaling)
         total_rays = rx * ry * rz
-        rays_per_gpu = total_rays // world
         launch = (rx, ry, rz)
     else:  # a fixed shard per rank (weak scaling)
-        rays_per_gpu = rx * ry * rz
-        total_rays = rays_per_gpu * world
+        total_rays = rx * ry * rz * world
         launch = (rx * world, ry, rz)
     settings = RenderSettings(rays=launch, ir_length_in_seconds=2, sample_rate=wl["sample_rate"],
                               base_power=3.62, max_bounces=wl["max_bounces"], hrtf_absorption_rate=1.0, seed=1,
                               device=local)
     scene = conference_standin()
     receiver = receiver_local()
-    r = AudioRenderer(settings, scene=scene, receiver=receiver)
-    r.setEmitterPosInOptix(CONFERENCE_EMITTER)
-    r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-    # one dedicated (non-null) stream for the renderer AND torch/RCCL, so the trace kernel,
-    # the all-reduce, the convolution and the timing events are ordered on it
+    if world > 1:  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
+        uid = [RenderGroup.unique_id() if rank == 0 else None]
+        D.broadcast_object(uid)
+        g = RenderGroup.rank(settings, world, rank, uid[0], scene=scene, receiver=receiver)
+    else:
+        g = RenderGroup(settings, devices=[local], scene=scene, receiver=receiver)
+    g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+    g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+    m = g.member(0)
+    # one dedicated (non-null) stream for the renderer, RCCL and the timing events
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    r.set_stream(stream.cuda_stream)
-    ir_len = r.ir_length
-    hist = torch.zeros(2 * ir_len, dtype=torch.int64, device=dev)
-    r.attach_histogram(hist.data_ptr(), hist.numel())
-    frames = wl["frames"]
-    audio = torch.from_numpy(synthetic_audio(frames, wl["sample_rate"], seed=rank)).to(dev)
+    m.set_stream(stream.cuda_stream)
+    ir_len = m.ir_length
+    audio_np, sr = reference_audio(wl["audio"])
+    assert sr == wl["sample_rate"]
+    frames = int(audio_np.size)
+    audio = torch.from_numpy(audio_np).to(dev)
     out_l = torch.empty_like(audio)
     out_r = torch.empty_like(audio)
-    b, e = D.shard_range(total_rays, rank, world)
 
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
     def step(k: int | None):
         if k is not None:
             ev[k][0].record(stream)
-        r.clear_histogram()
-        r.trace_rays(b, e)
+        g.render(timed=False)  # clear + trace + RCCL all-reduce + finalize
         if k is not None:
             ev[k][1].record(stream)
-        D.allreduce_histogram(hist)
-        r.finalize_ir()
+        m.convolute_device(audio.data_ptr(), frames, out_l.data_ptr(), out_r.data_ptr())
         if k is not None:
             ev[k][2].record(stream)
-        r.convolute_device(audio.data_ptr(), frames, out_l.data_ptr(), out_r.data_ptr())
-        if k is not None:
-            ev[k][3].record(stream)
 
     for _ in range(args.warmup):
         step(None)
     torch.cuda.synchronize(dev)
-    stats = r.stats()  # also raises if the kernel flagged a stack overflow
+    g.stats()
     D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -241,21 +299,24 @@ def main(argv=None) -> int:
     D.barrier()
     t1 = time.perf_counter()
     elapsed = D.max_over_ranks(t1 - t0, dev)
-    stats = r.stats()
+    stats = g.stats()
     q_rank = int(stats["queries"])  # per step (counters cleared every step)
     q_all = D.sum_over_ranks(q_rank, dev)
-    trace_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)]))
-    reduce_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)]))
-    conv_ms = float(np.mean([ev[k][2].elapsed_time(ev[k][3]) for k in range(args.steps)]))
-    trace_ms_max = D.max_over_ranks(trace_ms, dev)
+    # the trace kernel's own window (direction pre-pass + trace kernel, HIP events on the
+    # renderer's stream) for each of the K timed launches
+    trace_list = m.trace_times(args.steps)
+    trace_ms = float(np.mean(trace_list))
+    render_ms = float(np.mean([ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)]))
+    conv_ms = float(np.mean([ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)]))
     conv_ms_max = D.max_over_ranks(conv_ms, dev)
 
     value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
-    moving = moving_listener(r, D, dev, stream, hist, b, e, args.c5_frames) if args.c5_frames > 0 else None
+    moving = moving_listener(g, D, dev, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
     bpb = bytes_per_bounce(n_tris)
     achieved = q_rank * bpb / (trace_ms * 1e-3) / 1e9
-    traffic = load_traffic()
+    traffic = load_profile("trace_traffic.json")
+    counts = load_profile(os.path.join("r02", "trace_counts_c3.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
         "metric": METRIC,
@@ -270,22 +331,23 @@ def main(argv=None) -> int:
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: deterministic conference.obj stand-in (seed 42; conference.obj is missing from the "
-                "reference checkout) + synthetic 48 kHz audio",
+                "reference checkout) + the reference's own audio (" + wl["audio"] + ", channel 0)",
         "config": {
             "workload": wl["desc"],
             "scene_triangles": n_tris,
-            "rays_per_gpu": rays_per_gpu,
+            "rays_per_gpu": total_rays // world,
             "max_bounces": wl["max_bounces"],
             "sample_rate": wl["sample_rate"],
             "ir_len": ir_len,
             "audio_frames_per_gpu": frames,
-            "parallelism": f"ray-shard x{world}, RCCL int64 IR all-reduce" if world > 1 else "1 GPU",
+            "parallelism": f"ray-shard x{world}, native RCCL int64 IR all-reduce (arx_group)",
         },
         "ray_bounces_per_step": q_all,
         "nominal_ray_bounces_per_s": total_rays * wl["max_bounces"] * args.steps / elapsed,
         "receiver_hits_per_step_rank0": int(stats["receiver_hits"]),
         "convolved_frames_per_s": conv_frames_s,
-        "phases_ms_rank0": {"trace": trace_ms, "allreduce_finalize": reduce_ms, "ir_spectra_and_convolution": conv_ms},
+        "phases_ms_rank0": {"trace_kernel": trace_ms, "render_trace_allreduce_finalize": render_ms,
+                            "ir_spectra_and_convolution": conv_ms},
         "roofline": {
             "kernel": "trace_kernel",
             "bound": "hbm",
@@ -295,7 +357,10 @@ def main(argv=None) -> int:
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": (traffic or {}).get("bytes_per_launch") if traffic and traffic.get("workload") == args.workload
             else None,
+            "traffic_source": "profiles/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
+                              "and workload; PMC counters cannot be read inside this run)",
             "algorithmic_bytes_per_bounce": bpb,
+            "trace_launch_ms": trace_ms,
         },
         "roofline_convolution": {
             "bound": "hbm",
@@ -306,13 +371,29 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
         },
     }
+    if counts and args.workload == "c3":
+        lanes = counts["lane_loads_16B_per_query"] * q_rank
+        result["vector_memory"] = {
+            "node_steps_per_query": counts["steps_per_query"], "tri_tests_per_query": counts["tri_tests_per_query"],
+            "lane_loads_16B_per_query": counts["lane_loads_16B_per_query"],
+            "lane_loads_per_s": lanes / (trace_ms * 1e-3),
+            "l1_side_GBps": 16 * lanes / (trace_ms * 1e-3) / 1e9,
+            "source": "profiles/r02/trace_counts_c3.json (counting build, tools/trace_counts.py); TD busy per CU-cycle "
+                      "from rocprofv3 --pmc in profiles/r02/pmc_*.txt",
+        }
     if moving is not None:
         result["moving_listener"] = moving
+        if rank == 0 and world == 1 and not wl.get("total"):
+            shard = total_rays // 8
+            result["moving_listener_rank_of_8"] = moving_listener_rank_shape(settings, scene, receiver,
+                                                                             args.c5_frames, shard)
+    if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
+        result["streaming"] = streaming_leg(m, audio_np, 4096, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(scene, receiver, wl, total_rays, args.cpu_baseline_seconds)
+        result["cpu_baseline"] = cpu_baseline(scene, receiver, wl, total_rays, audio_np, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    r.close()
+    g.close()
     if world > 1:
         import torch.distributed as dist
 

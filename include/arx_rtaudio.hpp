@@ -8,9 +8,11 @@
 // functions match the typedef and can be passed to RtAudio::openStream directly.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstddef>
+#include <mutex>
 #include <vector>
 
 #include "arx.h"
@@ -21,35 +23,71 @@ namespace arx {
 constexpr unsigned kInputSampleRate = 44100;   // main.cpp:36
 constexpr unsigned kInputBufferLength = 4096;  // main.cpp:37
 
-// audioCallbackData (main.cpp:172-186) reduced to what the callback reads.
+// audioCallbackData (main.cpp:172-186) reduced to what the callback reads.  renderer_mutex (if
+// set) is the lock the render thread holds around render() / full_render_cycle: the callback only
+// try-locks it and outputs silence when the renderer is busy, so the two threads never drive the
+// renderer at once (arx.h: one host thread per renderer).  The reference instead checks a plain
+// bool is_rendering and then calls the renderer, a check-then-act race (main.cpp:104-112).
 struct MicCallbackData {
     arx_renderer* renderer = nullptr;
     CircularBuffer<double>* samplesRecordBuffer = nullptr;  // size 44100 * ir_sec (main.cpp:189)
     float volume = 1.0f;                                     // Context::get_volume()
     std::atomic<bool>* is_rendering = nullptr;               // Context::get_is_rendering()
+    std::mutex* renderer_mutex = nullptr;
     std::vector<double> scratch;                             // 2 * ir_len
+    arx_stream* stream = nullptr;                            // audio_handler_with_mic_stream only
 };
 
-// audioHandlerWithMic (main.cpp:99-135).
+// audioHandlerWithMic (main.cpp:99-135), the reference-compatible path: one full-length circular
+// convolution per callback added into the CircularBuffer.  At most min(nBufferFrames, 4096) input
+// frames are read (the reference always passes 4096, over-reading a smaller buffer).
 inline int audio_handler_with_mic(void* outputBuffer, void* inputBuffer, unsigned int nBufferFrames,
                                   double /*streamTime*/, unsigned int /*status*/, void* data) {
     MicCallbackData* d = static_cast<MicCallbackData*>(data);
     double* out = static_cast<double*>(outputBuffer);
     const double* in = static_cast<const double*>(inputBuffer);
-    if (d->is_rendering && d->is_rendering->load()) {  // "Buffer is still being processed"
-        for (unsigned i = 0; i < 2 * nBufferFrames; ++i) out[i] = 0.0;
+    std::unique_lock<std::mutex> lock;
+    if (d->renderer_mutex) lock = std::unique_lock<std::mutex>(*d->renderer_mutex, std::try_to_lock);
+    if ((d->is_rendering && d->is_rendering->load()) || (d->renderer_mutex && !lock.owns_lock())) {
+        for (unsigned i = 0; i < 2 * nBufferFrames; ++i) out[i] = 0.0;  // "Buffer is still being processed"
         return 0;
     }
     arx_config c;
     arx_get_config(d->renderer, &c);
     const size_t ir_len = (size_t)c.ir_length_in_seconds * (size_t)c.sample_rate;
     d->scratch.resize(2 * ir_len);
-    if (arx_convolute_live_block(d->renderer, in, kInputBufferLength * sizeof(double), d->scratch.data(),
-                                 d->scratch.size()) != ARX_OK)
+    const size_t n_in = std::min<size_t>(nBufferFrames, kInputBufferLength);
+    if (arx_convolute_live_block(d->renderer, in, n_in * sizeof(double), d->scratch.data(), d->scratch.size()) != ARX_OK)
         return 1;  // abort the stream on device failure (the reference would exit())
     d->samplesRecordBuffer->add(d->scratch.data(), d->scratch.size());
     std::vector<double> v = d->samplesRecordBuffer->get_and_reset(2 * (size_t)nBufferFrames);
     for (unsigned i = 0; i < 2 * nBufferFrames; ++i) out[i] = (v[i] != v[i]) ? 0.0 : v[i] * d->volume;
+    return 0;
+}
+
+// The same duplex callback over the streaming convolution (arx_stream_*, d->stream created with
+// block_frames = the stream's nBufferFrames): the output block is the linear convolution of the
+// mic stream with the IR, one block of latency, no circular wrap and no CircularBuffer.
+inline int audio_handler_with_mic_stream(void* outputBuffer, void* inputBuffer, unsigned int nBufferFrames,
+                                         double /*streamTime*/, unsigned int /*status*/, void* data) {
+    MicCallbackData* d = static_cast<MicCallbackData*>(data);
+    double* out = static_cast<double*>(outputBuffer);
+    const double* in = static_cast<const double*>(inputBuffer);
+    std::unique_lock<std::mutex> lock;
+    if (d->renderer_mutex) lock = std::unique_lock<std::mutex>(*d->renderer_mutex, std::try_to_lock);
+    int32_t block = 0;
+    if (!d->stream || arx_stream_info(d->stream, &block, nullptr, nullptr) != ARX_OK || nBufferFrames > (unsigned)block)
+        return 1;
+    if ((d->is_rendering && d->is_rendering->load()) || (d->renderer_mutex && !lock.owns_lock())) {
+        for (unsigned i = 0; i < 2 * nBufferFrames; ++i) out[i] = 0.0;
+        return 0;
+    }
+    d->scratch.resize(2 * (size_t)block);
+    if (arx_stream_process(d->stream, in, nBufferFrames, d->scratch.data(), d->scratch.size()) != ARX_OK) return 1;
+    for (unsigned i = 0; i < 2 * nBufferFrames; ++i) {
+        const double v = d->scratch[i];
+        out[i] = (v != v) ? 0.0 : v * d->volume;
+    }
     return 0;
 }
 

@@ -21,7 +21,7 @@ class OrcParams(C.Structure):
         ("ir_length", C.c_int32), ("sample_rate", C.c_int32),
         ("base_power", C.c_float), ("energy_thres", C.c_float), ("max_bounces", C.c_uint32),
         ("hrtf_absorption_rate", C.c_float), ("is_mono", C.c_int32), ("seed", C.c_uint64),
-        ("emitter", C.c_float * 3), ("sphere_center", C.c_float * 3),
+        ("emitter", C.c_float * 3), ("sphere_center", C.c_float * 3), ("arith", C.c_int32),
     ]
 
 
@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
         I64 = C.POINTER(C.c_int64)
         L.orc_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.orc_ray_direction.argtypes = [C.c_uint64, C.c_uint64, F]
+        L.orc_ray_direction_reference.argtypes = [C.c_uint64, C.c_uint64, F]
         L.orc_initial_energy.argtypes = [C.POINTER(OrcParams)]
         L.orc_initial_energy.restype = C.c_float
         L.orc_frac_bits.argtypes = [C.c_uint64]
@@ -102,11 +103,12 @@ def philox(ctr, key):
     return [int(x) for x in o]
 
 
-def ray_directions(seed: int, first: int, count: int) -> np.ndarray:
+def ray_directions(seed: int, first: int, count: int, reference_formula: bool = False) -> np.ndarray:
+    fn = lib().orc_ray_direction_reference if reference_formula else lib().orc_ray_direction
     out = np.empty((count, 3), np.float32)
     row = (C.c_float * 3)()
     for i in range(count):
-        lib().orc_ray_direction(seed, first + i, row)
+        fn(seed, first + i, row)
         out[i] = row[:]
     return out
 
@@ -117,7 +119,7 @@ def frac_bits(n: int) -> int:
 
 def make_params(*, rays=(32, 32, 1), sample_rate=16000, ir_seconds=2, base_power=3.62, energy_thres=0.0,
                 max_bounces=2, hrtf=1.0, mono=False, seed=1, emitter=(0.0, 0.0, 0.0),
-                listener=(2.5, 9.9, 0.0)) -> OrcParams:
+                listener=(2.5, 9.9, 0.0), arith: int = 0) -> OrcParams:
     p = OrcParams()
     p.rays_x, p.rays_y, p.rays_z = rays
     p.sample_rate = sample_rate
@@ -128,6 +130,7 @@ def make_params(*, rays=(32, 32, 1), sample_rate=16000, ir_seconds=2, base_power
     p.hrtf_absorption_rate = hrtf
     p.is_mono = 1 if mono else 0
     p.seed = seed
+    p.arith = int(arith)
     p.emitter[:] = list(emitter)
     p.sphere_center[:] = list(listener)
     return p
