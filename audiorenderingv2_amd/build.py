@@ -24,7 +24,7 @@ OBJDIR = os.path.join(PKG, "_obj")
 LIB = os.path.join(PKG, "libarx.so")
 ARCH = os.environ.get("ARX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["arx_trace.hip", "arx_conv.hip", "arx_capi.cpp", "arx_group.cpp", "arx_bvh.cpp", "arx_io.cpp"]
+SOURCES = ["arx_trace.hip", "arx_receiver.hip", "arx_conv.hip", "arx_capi.cpp", "arx_group.cpp", "arx_bvh.cpp", "arx_io.cpp"]
 HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp"]
 
 COMMON = [

@@ -70,7 +70,6 @@ bool validate_bvh_range(const BvhNode* nodes, size_t first, size_t n_nodes, size
 // entry format), or kEmptyChildCode for an empty child: a leaf of 0 triangles, i.e. a no-op if
 // its inverted box ever passes the slab test (-1 is kept free: it means "no entry").  Boxes are
 // unchanged.
-constexpr int32_t kEmptyChildCode = ~16;
 void code_nodes(const BvhNode* in, size_t n, BvhNode* out);
 // Grid for QNode2 trees covering the box [lo, hi] (scene, receiver and emitter) with a margin
 // of margin_frac of the largest extent on every side, so listener moves inside the room keep

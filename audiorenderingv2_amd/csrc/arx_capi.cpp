@@ -90,10 +90,109 @@ void place_vertices(const float* local, int64_t n_vertices, float x, float y, fl
     }
 }
 
+// Rotation of place_vertices (row-major r00 r10 r20 / r01 r11 r21 / r02 r12 r22), exactly its floats.
+void receiver_rotation(float yaw_deg, float m[9]) {
+    const float ang = yaw_deg * static_cast<float>(0.01745329251994329576923690768489);
+    const float a = -ang, c = std::cos(a), s = std::sin(a), t1 = 1.0f - c;
+    m[0] = c + 0.0f * 0.0f; m[1] = t1 * 0.0f - s * 0.0f; m[2] = 0.0f * 0.0f + s * 1.0f;
+    m[3] = 0.0f * 1.0f + s * 0.0f; m[4] = c + t1 * 1.0f; m[5] = 0.0f * 1.0f - s * 0.0f;
+    m[6] = 0.0f * 0.0f - s * 1.0f; m[7] = t1 * 0.0f + s * 0.0f; m[8] = c + 0.0f * 0.0f;
+}
+
+// The receiver sub-tree, built once in the receiver's local frame whenever the receiver model or
+// the scene changes (its triangle ids and offsets follow the scene); listener moves refit it on
+// the device (arx_receiver.hip).  Larger receivers than the refit kernel's LDS holds are rebuilt on
+// the host per move instead (recv_refit = false).
+arx_status prepare_receiver_model(arx_renderer* r) {
+    std::vector<float> tv, ab;
+    float radius = 0.0f;
+    for (int side = 0; side < 2; ++side) {
+        const std::vector<float>& loc = r->recv_local[side];
+        tv.insert(tv.end(), loc.begin(), loc.end());
+        ab.insert(ab.end(), loc.size() / 9, side == 0 ? -1.0f : -2.0f);
+        for (size_t i = 0; i + 2 < loc.size(); i += 3)
+            radius = std::max(radius, std::sqrt(loc[i] * loc[i] + loc[i + 1] * loc[i + 1] + loc[i + 2] * loc[i + 2]));
+    }
+    const int64_t n = (int64_t)ab.size();
+    r->recv_refit = n <= kRefitMaxTris;
+    r->recv_radius = radius * 1.0001f + 1e-6f;  // |R v| = |v|: the rotated halves stay in this ball
+    if (!r->recv_refit) return ARX_OK;
+    build_bvh(tv.data(), ab.data(), 0.0f, n, (int32_t)r->n_scene, r->recv);
+    relocate_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), (int32_t)r->scene.tris.size());
+    const char* why = "";
+    const size_t total_nodes = 1 + r->scene.nodes.size() + r->recv.nodes.size();
+    const size_t total_tris = r->scene.tris.size() + r->recv.tris.size();
+    if (!validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(), total_nodes,
+                            total_tris, &why))
+        return fail(ARX_ERR_INTERNAL, "BVH validation failed (receiver): %s", why);
+    // refit schedule: inner nodes by depth, deepest level first
+    const int32_t base = 1 + (int32_t)r->scene.nodes.size();
+    std::vector<int32_t> depth(r->recv.nodes.size(), 0);
+    int32_t max_d = 0;
+    for (size_t i = 0; i < r->recv.nodes.size(); ++i)  // parents precede children (pre-order)
+        for (int c = 0; c < 2; ++c)
+            if (r->recv.nodes[i].d[2 + c] == 0) {
+                const int32_t ch = r->recv.nodes[i].d[c] - base;
+                depth[(size_t)ch] = depth[i] + 1;
+                max_d = std::max(max_d, depth[(size_t)ch]);
+            }
+    std::vector<int32_t> order, start;
+    for (int32_t d = max_d; d >= 0 && !r->recv.nodes.empty(); --d) {
+        start.push_back((int32_t)order.size());
+        for (size_t i = 0; i < r->recv.nodes.size(); ++i)
+            if (depth[i] == d) order.push_back((int32_t)i);
+    }
+    start.push_back((int32_t)order.size());
+    r->recv_levels = r->recv.nodes.empty() ? 0 : (int32_t)start.size() - 1;
+    hipFree(r->d_recv_local);
+    hipFree(r->d_recv_nodes);
+    hipFree(r->d_recv_levels);
+    r->d_recv_local = nullptr;
+    r->d_recv_nodes = nullptr;
+    r->d_recv_levels = nullptr;
+    ARX_HIP(hipMalloc(&r->d_recv_local, std::max<size_t>(1, r->recv.tris.size()) * sizeof(TriRec)));
+    ARX_HIP(hipMalloc(&r->d_recv_nodes, std::max<size_t>(1, r->recv.nodes.size()) * sizeof(BvhNode)));
+    ARX_HIP(hipMalloc(&r->d_recv_levels, (order.size() + start.size()) * sizeof(int32_t)));
+    if (!r->recv.tris.empty())
+        ARX_HIP(hipMemcpyAsync(r->d_recv_local, r->recv.tris.data(), r->recv.tris.size() * sizeof(TriRec),
+                               hipMemcpyHostToDevice, r->stream));
+    if (!r->recv.nodes.empty())
+        ARX_HIP(hipMemcpyAsync(r->d_recv_nodes, r->recv.nodes.data(), r->recv.nodes.size() * sizeof(BvhNode),
+                               hipMemcpyHostToDevice, r->stream));
+    std::vector<int32_t> lv(order);
+    lv.insert(lv.end(), start.begin(), start.end());
+    ARX_HIP(hipMemcpyAsync(r->d_recv_levels, lv.data(), lv.size() * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
+    ARX_HIP(hipStreamSynchronize(r->stream));  // pageable sources
+    r->recv_level_count = (int32_t)order.size();
+    return ARX_OK;
+}
+
+// World-space bound of the placed receiver (for the quantization grid): the refit path's ball, or
+// the host-built sub-tree's root box.
+void receiver_bound(const arx_renderer* r, float lo[3], float hi[3], bool* empty) {
+    *empty = (r->recv_local[0].size() + r->recv_local[1].size()) == 0;
+    for (int k = 0; k < 3; ++k) {
+        if (r->recv_refit) {
+            lo[k] = r->center[k] - r->recv_radius;
+            hi[k] = r->center[k] + r->recv_radius;
+        } else {
+            lo[k] = r->recv.root.lo[k];
+            hi[k] = r->recv.root.hi[k];
+        }
+    }
+}
+
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_set) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
-    if (r->recv_dirty) {
-        // receiver halves placed in world space, left then right (placeReceiver OptixModel.cpp:153-157)
+    const bool model_changed = r->recv_model_dirty || r->scene_dirty;
+    if (model_changed) {
+        arx_status st = prepare_receiver_model(r);
+        if (st != ARX_OK) return st;
+    }
+    const bool pose_changed = model_changed || r->recv_pose_dirty;
+    if (!r->recv_refit && pose_changed) {
+        // host path (receivers beyond the refit kernel's capacity): receiver halves placed in world
+        // space, left then right (placeReceiver OptixModel.cpp:153-157), sub-tree rebuilt
         std::vector<float> tv;
         std::vector<float> ab;
         for (int side = 0; side < 2; ++side) {
@@ -137,17 +236,22 @@ arx_status ensure_device_scene(arx_renderer* r) {
     // grid spans the old one, the scene, the receiver and the emitter with half the extent as
     // margin, so such a walk re-grids once or twice, not per frame.  An emitter off the grid
     // (checked per launch, arx_trace_rays) makes the launches take the f32 nodes instead.
-    const bool grow = !full && r->qgrid_set && r->recv_dirty && r->recv.root.count >= 0 &&
-                      !qgrid_contains(r->qgrid, r->recv.root.lo, r->recv.root.hi);
+    float rlo[3], rhi[3];
+    bool recv_empty = false;
+    receiver_bound(r, rlo, rhi, &recv_empty);
+    const bool grow = !full && r->qgrid_set && pose_changed && !recv_empty && !qgrid_contains(r->qgrid, rlo, rhi);
     const bool requant = full || !r->qgrid_set || grow;
     if (requant) {
         float lo[3], hi[3];
         for (int k = 0; k < 3; ++k) {
             lo[k] = hi[k] = r->emitter[k];
-            for (const ChildRef* c : {&r->scene.root, &r->recv.root}) {
-                if (c->count < 0) continue;  // empty part
-                lo[k] = std::min(lo[k], c->lo[k]);
-                hi[k] = std::max(hi[k], c->hi[k]);
+            if (r->scene.root.count >= 0) {
+                lo[k] = std::min(lo[k], r->scene.root.lo[k]);
+                hi[k] = std::max(hi[k], r->scene.root.hi[k]);
+            }
+            if (!recv_empty) {
+                lo[k] = std::min(lo[k], rlo[k]);
+                hi[k] = std::max(hi[k], rhi[k]);
             }
             if (grow) {
                 lo[k] = std::min(lo[k], r->qgrid.origin[k]);
@@ -157,24 +261,26 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->qgrid = make_qgrid(lo, hi, grow ? 0.5 : 0.1);
         r->qgrid_set = true;
     }
-    if (full || r->recv_dirty || requant) {
-        BvhNode top = make_node(r->scene.root, r->recv.root);
+    const bool recv_on_grid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
+    if (full || requant || (!r->recv_refit && pose_changed) || (r->recv_refit && model_changed)) {
+        // host uploads: the top node (its receiver child comes from the refit kernel on the refit
+        // path), the scene part when it changed, the receiver part on the host path
+        const bool host_recv = !r->recv_refit;
+        BvhNode top = make_node(r->scene.root, host_recv ? r->recv.root : empty_child());
         {
-            // structure check (acyclic, in range): the scene part when it changed, the receiver
-            // part and the top node on every listener move
             const char* why = "";
             if (full && !validate_bvh_range(r->scene.nodes.data(), 1, r->scene.nodes.size(), n_nodes, n_tris, &why))
                 return fail(ARX_ERR_INTERNAL, "BVH validation failed (scene): %s", why);
-            if (!validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(), n_nodes,
-                                    n_tris, &why) ||
+            if ((host_recv && !validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(),
+                                                  n_nodes, n_tris, &why)) ||
                 !validate_bvh_range(&top, 0, 1, n_nodes, n_tris, &why))
                 return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
         }
         // coded copies of the parts being uploaded (kept in host vectors that live until the sync)
         BvhNode ctop;
         code_nodes(&top, 1, &ctop);
-        std::vector<BvhNode> cscene, crecv(r->recv.nodes.size());
-        code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
+        std::vector<BvhNode> cscene, crecv(host_recv ? r->recv.nodes.size() : 0);
+        if (host_recv) code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
         ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
         r->qtop_h.assign(1, QNode2{});
         r->qrecv_h.assign(crecv.size(), QNode2{});
@@ -198,22 +304,53 @@ arx_status ensure_device_scene(arx_renderer* r) {
         if (full && !r->scene.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
                                    hipMemcpyHostToDevice, r->stream));
-        if (!r->recv.nodes.empty()) {
+        if (host_recv && !r->recv.nodes.empty()) {
             ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
                                    crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
             if (q_ok)
                 ARX_HIP(hipMemcpyAsync(r->d_qnodes + 1 + r->scene.nodes.size(), r->qrecv_h.data(),
                                        r->qrecv_h.size() * sizeof(QNode2), hipMemcpyHostToDevice, r->stream));
         }
-        if (!r->recv.tris.empty())
+        if (host_recv && !r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
                                    r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
-        r->q_valid = q_ok;
+        r->q_valid = q_ok && recv_on_grid;
         // the host vectors are pageable: make sure the copies are done before they can change
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
+    if (r->recv_refit && (pose_changed || full || requant)) {
+        // the listener move itself: one kernel, no host copies, no synchronisation
+        RefitArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.local_tris = r->d_recv_local;
+        a.n_tris = (int32_t)r->recv.tris.size();
+        a.tri_base = (int32_t)r->scene.tris.size();
+        a.local_nodes = r->d_recv_nodes;
+        a.n_nodes = (int32_t)r->recv.nodes.size();
+        a.node_base = 1 + (int32_t)r->scene.nodes.size();
+        a.level_nodes = r->d_recv_levels;
+        a.level_start = r->d_recv_levels + r->recv_level_count;
+        a.n_levels = r->recv_levels;
+        a.root_ref = r->recv.root.ref;
+        a.root_count = r->recv.root.count;
+        receiver_rotation(r->yaw, a.m);
+        float mx = 0.0f;
+        for (int k = 0; k < 3; ++k) {
+            a.t[k] = r->center[k];
+            mx = std::max(mx, std::fabs(r->center[k]));
+        }
+        a.pad = std::max(1e-5f * (mx + r->recv_radius) * 1.001f, 1e-6f);  // >= the builder's pad
+        a.grid = r->qgrid;
+        a.tris = r->d_tris;
+        a.cnodes = r->d_cnodes;
+        a.qnodes = recv_on_grid ? r->d_qnodes : nullptr;
+        a.flag = reinterpret_cast<unsigned int*>(r->d_counters + 6);
+        if (a.n_tris > 0) ARX_HIP(launch_receiver_refit(a, r->stream));
+        r->q_valid = r->q_valid && recv_on_grid;
+    }
     r->scene_dirty = false;
-    r->recv_dirty = false;
+    r->recv_model_dirty = false;
+    r->recv_pose_dirty = false;
     r->stats.n_scene_tris = r->n_scene;
     r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
     r->stats.n_nodes = (int64_t)n_nodes;
@@ -355,6 +492,9 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_tris);
     hipFree(r->d_gstack);
     hipFree(r->d_dirs);
+    hipFree(r->d_recv_local);
+    hipFree(r->d_recv_nodes);
+    hipFree(r->d_recv_levels);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
@@ -397,7 +537,7 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
     r->n_scene = n;
     r->scene_set = true;
     r->scene_dirty = true;
-    r->recv_dirty = true;  // receiver ids and offsets follow the scene
+    r->recv_model_dirty = true;  // receiver ids and offsets follow the scene
     return ARX_OK;
 }
 
@@ -405,7 +545,7 @@ arx_status arx_set_receiver_model(arx_renderer* r, int side, const float* tri_v,
     if (!r || side < 0 || side > 1 || n < 0 || (n > 0 && !tri_v))
         return fail(ARX_ERR_INVALID_ARGUMENT, "bad receiver model arguments");
     r->recv_local[side].assign(tri_v, tri_v + 9 * n);
-    r->recv_dirty = true;
+    r->recv_model_dirty = true;
     return ARX_OK;
 }
 
@@ -431,7 +571,7 @@ arx_status arx_set_listener(arx_renderer* r, float x, float y, float z, float ya
     r->center[1] = y;
     r->center[2] = z;
     r->yaw = yaw_deg;
-    r->recv_dirty = true;
+    r->recv_pose_dirty = true;
     return ARX_OK;
 }
 
@@ -620,6 +760,7 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     float cms = 0.f;
     if (r->conv_launches > 0 && hipEventElapsedTime(&cms, r->cev0, r->cev1) == hipSuccess) r->stats.conv_ms = cms;
     *out = r->stats;
+    if (r->h_counters[6]) return fail(ARX_ERR_INTERNAL, "receiver refit: a box left the quantization grid");
     return ARX_OK;
 }
 

@@ -25,8 +25,12 @@ arx_status fail(arx_status s, const char* fmt, ...) __attribute__((format(printf
                                "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__);   \
     } while (0)
 
-// device counters: [0] queries [1] receiver hits [2] misses [3] error flag
+// device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4..5] counting builds
+// [6] receiver refit left the quantization grid
 constexpr int kCounters = 8;
+// receivers up to this many triangles are moved by the device refit (its LDS holds 9 floats per
+// triangle and 6 per node); larger ones are rebuilt on the host per move
+constexpr int64_t kRefitMaxTris = 3000;
 
 inline uint64_t n_rays(const arx_config& c) {
     return (uint64_t)(int64_t)c.rays_x * (uint64_t)(int64_t)c.rays_y * (uint64_t)(int64_t)c.rays_z;
@@ -66,8 +70,16 @@ struct arx_renderer {
     std::vector<float> recv_local[2];
     arx::BvhBuild recv;
     bool scene_dirty = true;
-    bool recv_dirty = true;
+    bool recv_model_dirty = true;  // receiver halves or scene changed: rebuild the local sub-tree
+    bool recv_pose_dirty = true;   // listener moved: refit on the device
     bool scene_set = false;
+    // receiver sub-tree in its local frame (refit path) and its device images
+    bool recv_refit = true;
+    float recv_radius = 0.0f;
+    arx::TriRec* d_recv_local = nullptr;
+    arx::BvhNode* d_recv_nodes = nullptr;
+    int32_t* d_recv_levels = nullptr;  // level-ordered node indices, then level starts
+    int32_t recv_levels = 0, recv_level_count = 0;
 
     // device
     arx::BvhNode* d_cnodes = nullptr;  // coded copy of the tree (code_nodes): the f32 fallback

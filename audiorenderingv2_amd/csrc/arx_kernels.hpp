@@ -22,6 +22,30 @@ hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_r
 hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hipStream_t s);
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
 
+// ---- moving listener (arx_receiver.hip): transform + fixed-topology refit of the receiver ----
+struct RefitArgs {
+    const TriRec* local_tris;   // receiver triangles in leaf order, local frame (ids, absorption set)
+    int32_t n_tris;
+    int32_t tri_base;           // global TriRec index of the first receiver triangle
+    const BvhNode* local_nodes; // receiver sub-tree (relocated: global refs), boxes unused
+    int32_t n_nodes;
+    int32_t node_base;          // global node index of local node 0
+    const int32_t* level_nodes; // local node indices, deepest level first
+    const int32_t* level_start; // [n_levels + 1] offsets into level_nodes
+    int32_t n_levels;
+    int32_t root_ref, root_count;  // the receiver root as a child reference (global)
+    float m[9];                 // rotation, row-major in place_vertices' order (r00 r10 r20, r01 r11 r21, r02 r12 r22)
+    float t[3];                 // listener position
+    float pad;                  // box padding (>= the builder's 1e-5 * max|coordinate|)
+    QGrid grid;
+    TriRec* tris;               // outputs
+    BvhNode* cnodes;
+    QNode2* qnodes;             // null: the quantized copy is not maintained (receiver off the grid)
+    unsigned int* flag;         // set if a box fell off the grid (never, given the host's bound)
+};
+size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes);
+hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
+
 // ---- convolution (arx_conv.hip) ----
 struct ConvPlan;  // opaque, defined in arx_conv.hip
 ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char* err, size_t errlen);

@@ -52,6 +52,10 @@ struct alignas(16) QNode2 {
 };
 static_assert(sizeof(QNode2) == 32, "QNode2 must be 32 B");
 
+// Stack-entry / child code of an empty child in the coded and quantized nodes (code_nodes,
+// arx_bvh.hpp): a leaf of 0 triangles (-1 is kept free: it means "no entry").
+constexpr int32_t kEmptyChildCode = ~16;
+
 // The scene-wide grid of QNode2 trees.
 struct QGrid {
     float origin[3];

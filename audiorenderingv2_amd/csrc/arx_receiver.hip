@@ -1,0 +1,156 @@
+// arx_receiver.hip -- moving-listener update on the device.
+//
+// The reference re-places the receiver half-spheres on the host (place_receiver_half,
+// OptixModel.cpp:159-257) and then rebuilds the whole GAS, pipeline and SBT (reload,
+// AudioRenderer.cpp:466-486) for every listener move.  Here the receiver sub-tree is built ONCE in
+// the receiver's local frame (arx_capi.cpp, when the receiver model or the scene changes); a move
+// is one kernel launch on the renderer's stream, with no host work beyond its arguments:
+//   1. every receiver triangle is transformed to world space with place_receiver_half's exact
+//      operation order (the vertex transform of OptixModel.cpp:178-193, glm::rotate about +Y by
+//      -yaw, then + listener position) and written to its TriRec slot;
+//   2. the sub-tree's boxes are refit bottom-up, level by level (fixed topology), padded, and
+//      written as the coded f32 node (the fallback format) and the 16-bit quantized node;
+//   3. the top node's receiver child is rewritten from the refit root box.
+// The closest hit does not depend on the tree (any conservative tree gives the same hit and
+// tie-break), so the result stays bit-exact with the oracle, which builds its own tree.
+#include <hip/hip_runtime.h>
+
+#include "arx_kernels.hpp"
+#include "arx_layout.hpp"
+
+namespace arx {
+namespace {
+
+constexpr int kRefitThreads = 256;
+
+__device__ __forceinline__ int32_t child_code(int32_t ref, int32_t count) {
+    return count < 0 ? kEmptyChildCode : count == 0 ? ref : ~(ref * 16 + count);  // code_nodes (arx_bvh.cpp)
+}
+
+// Outward 16-bit grid index of a plane with the 0.1-step margin (quantize_nodes16, arx_bvh.cpp).
+__device__ __forceinline__ bool quantize_axis(const QGrid& g, int k, float lo, float hi, uint32_t& word) {
+    const double l = floor(((double)lo - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
+    const double h = ceil(((double)hi - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
+    if (!(l >= 0.0) || !(h <= 65535.0)) return false;
+    word = (uint32_t)l | ((uint32_t)h << 16);
+    return true;
+}
+
+// Box (lo, hi) of child c, unpadded, into the node's coded f32 form (padded) and its quantized half.
+__device__ void write_child(const RefitArgs& a, int32_t node, int c, const float* lo, const float* hi, int32_t code,
+                            bool empty) {
+    BvhNode* n = a.cnodes + node;
+    float* ab = c == 0 ? n->a : n->b;
+    if (empty) {  // the inverted box of empty_child(): never passes the slab test
+        ab[0] = 1e30f; ab[1] = -1e30f; ab[2] = 1e30f; ab[3] = -1e30f;
+        n->c[2 * c] = 1e30f;
+        n->c[2 * c + 1] = -1e30f;
+    } else {
+        ab[0] = lo[0] - a.pad; ab[1] = hi[0] + a.pad; ab[2] = lo[1] - a.pad; ab[3] = hi[1] + a.pad;
+        n->c[2 * c] = lo[2] - a.pad;
+        n->c[2 * c + 1] = hi[2] + a.pad;
+    }
+    n->d[c] = code;
+    if (!a.qnodes) return;
+    QChild& q = a.qnodes[node].c[c];
+    for (int k = 0; k < 3; ++k) {
+        uint32_t w = 1u;  // empty: the slab between planes 0 and 1 (quantize_nodes16)
+        if (!empty && !quantize_axis(a.grid, k, lo[k] - a.pad, hi[k] + a.pad, w)) {
+            atomicOr(a.flag, 1u);  // off the grid: the host's bound should have prevented it
+            w = 0u | (65535u << 16);
+        }
+        q.q[k] = w;
+    }
+    q.code = code;
+}
+
+__global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs a) {
+    extern __shared__ float lds[];
+    float* wv = lds;                   // world vertices, 9 per receiver triangle
+    float* nb = lds + 9 * a.n_tris;    // node boxes (lo xyz, hi xyz), unpadded
+    // 1. transform (OptixModel.cpp:178-193 with glm's operation order, as arx_place_receiver_vertices)
+    for (int i = threadIdx.x; i < a.n_tris; i += kRefitThreads) {
+        const TriRec src = a.local_tris[i];
+        TriRec dst = src;
+        const float* v[3] = {src.v0, src.v1, src.v2};
+        float* o[3] = {dst.v0, dst.v1, dst.v2};
+        for (int j = 0; j < 3; ++j) {
+            const float vx = v[j][0], vy = v[j][1], vz = v[j][2];
+            const float ox = (a.m[0] * vx + a.m[1] * vy) + (a.m[2] * vz + 0.0f);
+            const float oy = (a.m[3] * vx + a.m[4] * vy) + (a.m[5] * vz + 0.0f);
+            const float oz = (a.m[6] * vx + a.m[7] * vy) + (a.m[8] * vz + 0.0f);
+            o[j][0] = a.t[0] + ox;
+            o[j][1] = a.t[1] + oy;
+            o[j][2] = a.t[2] + oz;
+            wv[9 * i + 3 * j + 0] = o[j][0];
+            wv[9 * i + 3 * j + 1] = o[j][1];
+            wv[9 * i + 3 * j + 2] = o[j][2];
+        }
+        a.tris[a.tri_base + i] = dst;
+    }
+    __syncthreads();
+    // box of a child reference (global refs): a leaf's triangles or an already refit node
+    auto child_box = [&](int32_t ref, int32_t count, float* lo, float* hi) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = __builtin_huge_valf();
+            hi[k] = -__builtin_huge_valf();
+        }
+        if (count > 0) {
+            for (int32_t t = ref - a.tri_base; t < ref - a.tri_base + count; ++t)
+                for (int j = 0; j < 3; ++j)
+                    for (int k = 0; k < 3; ++k) {
+                        lo[k] = fminf(lo[k], wv[9 * t + 3 * j + k]);
+                        hi[k] = fmaxf(hi[k], wv[9 * t + 3 * j + k]);
+                    }
+        } else if (count == 0) {
+            const float* b = nb + 6 * (ref - a.node_base);
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = b[k];
+                hi[k] = b[3 + k];
+            }
+        }
+    };
+    // 2. bottom-up refit, deepest level first (fixed topology)
+    for (int L = 0; L < a.n_levels; ++L) {
+        for (int i = a.level_start[L] + threadIdx.x; i < a.level_start[L + 1]; i += kRefitThreads) {
+            const int32_t ln = a.level_nodes[i];
+            const BvhNode src = a.local_nodes[ln];
+            float blo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
+            float bhi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
+            for (int c = 0; c < 2; ++c) {
+                const int32_t ref = src.d[c], count = src.d[2 + c];
+                float lo[3], hi[3];
+                child_box(ref, count, lo, hi);
+                write_child(a, a.node_base + ln, c, lo, hi, child_code(ref, count), count < 0);
+                for (int k = 0; k < 3; ++k) {
+                    blo[k] = fminf(blo[k], lo[k]);
+                    bhi[k] = fmaxf(bhi[k], hi[k]);
+                }
+            }
+            for (int k = 0; k < 3; ++k) {
+                nb[6 * ln + k] = blo[k];
+                nb[6 * ln + 3 + k] = bhi[k];
+            }
+        }
+        __syncthreads();
+    }
+    // 3. the top node's receiver child (child 1) from the root
+    if (threadIdx.x == 0) {
+        float lo[3], hi[3];
+        child_box(a.root_ref, a.root_count, lo, hi);
+        write_child(a, 0, 1, lo, hi, child_code(a.root_ref, a.root_count), a.root_count < 0);
+    }
+}
+
+}  // namespace
+
+size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes) { return ((size_t)9 * n_tris + (size_t)6 * n_nodes) * 4; }
+
+hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(receiver_refit_kernel, dim3(1), dim3(kRefitThreads), receiver_refit_lds(a.n_tris, a.n_nodes), s,
+                       a);
+    return hipGetLastError();
+}
+
+}  // namespace arx

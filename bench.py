@@ -73,7 +73,7 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> d
     osc = po.Scene(tv, ta, bvh=True)
     p = po.make_params(rays=(n_total_rays, 1, 1), sample_rate=wl["sample_rate"], base_power=3.62,
                        max_bounces=wl["max_bounces"], emitter=CONFERENCE_EMITTER, listener=CONFERENCE_LISTENER)
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = available_cores()
 
     def timed(threads: int, seconds: float) -> tuple[float, int, float]:
         n = 500 * threads
@@ -100,12 +100,27 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> d
     return {
         "value": allc, "unit": "ray-bounces/s", "cores": cores, "kind": "port",
         "sample": f"oracle/arx_oracle.c (-O3, median-split BVH): rays 0..{n2} of the same launch on {cores} "
-                  f"threads ({d2:.1f} s); 1 thread: rays 0..{n1} ({d1:.1f} s)",
+                  f"threads = the CPUs this process may use (affinity capped by the cgroup quota) ({d2:.1f} s); "
+                  f"1 thread: rays 0..{n1} ({d1:.1f} s)",
         "single_thread_value": one,
         "convolved_frames_per_s": x.size / (dtc / 2),
         "convolution_sample": f"f64 oracle block convolution, 1 thread, {x.size} frames x 2 ears",
         "cpu_model": _cpu_model(),
     }
+
+
+def available_cores() -> int:
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota (on the GPU box the
+    mask lists the whole machine while the container's share is a fraction of it)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _cpu_model() -> str:
