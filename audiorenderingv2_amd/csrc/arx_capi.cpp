@@ -54,6 +54,8 @@ arx_status check_config(const arx_config* c) {
     if ((uint64_t)c->rays_x * (uint64_t)c->rays_y * (uint64_t)c->rays_z > 0x7fffffffull)
         return fail(ARX_ERR_INVALID_ARGUMENT, "x*y*z must fit int32 (devicePrograms.cu:208 int product)");
     if (c->sample_rate <= 0) return fail(ARX_ERR_INVALID_ARGUMENT, "sample_rate must be positive");
+    if (!(c->hrtf_absorption_rate >= 0.0f && c->hrtf_absorption_rate <= 1.0f))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "hrtf_absorption_rate must be in [0, 1]");
     if (c->ir_length_in_seconds == 0) return fail(ARX_ERR_INVALID_ARGUMENT, "ir_length_in_seconds must be >= 1");
     const uint64_t L = (uint64_t)c->ir_length_in_seconds * (uint64_t)c->sample_rate;
     if (L > 0x7fffffffull) return fail(ARX_ERR_INVALID_ARGUMENT, "ir length too large");
@@ -531,6 +533,14 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
     if (n > (int64_t)0x3fffffff) return fail(ARX_ERR_INVALID_ARGUMENT, "too many triangles");
     for (int64_t i = 0; i < 9 * n; ++i)
         if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
+    // absorption in [0, 1], or the receiver marks -1 / -2 (getMaterialAbsorption): the int64
+    // fixed-point histogram's headroom (arx_frac_bits) assumes a ray's energy never grows
+    for (int64_t i = 0; i < n; ++i) {
+        const float ab = tri_abs[i];
+        if (!(ab >= 0.0f && ab <= 1.0f) && ab != -1.0f && ab != -2.0f)
+            return fail(ARX_ERR_INVALID_ARGUMENT, "absorption %g of triangle %lld: must be in [0, 1] (or -1 / -2 receiver)",
+                        (double)ab, (long long)i);
+    }
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
     bfs_prefix_order(r->scene, 1023);  // the top levels of the scene tree breadth-first (node locality)
     relocate_bvh(r->scene, 1, 0);
@@ -584,6 +594,8 @@ arx_status arx_set_thresholds(arx_renderer* r, float energy, uint32_t max_bounce
 
 arx_status arx_set_hrtf_absorption_rate(arx_renderer* r, float v) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (!(v >= 0.0f && v <= 1.0f))  // the cross-ear factor (1 - hrtf) stays in [0, 1] (histogram headroom)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "hrtf_absorption_rate %g must be in [0, 1]", (double)v);
     r->cfg.hrtf_absorption_rate = v;
     return ARX_OK;
 }

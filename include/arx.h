@@ -85,7 +85,9 @@ void* arx_get_stream(const arx_renderer* r);
  * with getMaterialAbsorption (:34-56) already applied per triangle by the caller
  * (arx_material_absorption).  tri_vertices: n_tris*9 floats (P1,P2,P3 in mesh index order);
  * triangle order is the global id used to break equal-distance ties.  Builds the
- * SAH BVH on the host and uploads it (once; receivers are kept in a separate sub-tree). */
+ * SAH BVH on the host and uploads it (once; receivers are kept in a separate sub-tree).
+ * Absorption must lie in [0, 1] (or be -1 / -2, the receiver marks): unlike the reference, which
+ * takes any config value, the int64 fixed-point IR needs energies that never grow. */
 arx_status arx_set_scene(arx_renderer* r, const float* tri_vertices, const float* tri_absorption,
                          int64_t n_tris);
 /* The two receiver half-spheres in their local frame: HalfSphere (HalfSphere.cpp:3-31) loaded

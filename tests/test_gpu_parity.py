@@ -388,3 +388,20 @@ def test_convolution_device_api_equals_host_api():
     import audiorenderingv2_amd._lib as L_
     L_.check(L_.lib().arx_copy_ir(r.handle, None, None, r.ir_length))  # syncs the renderer stream
     assert np.array_equal(dl.cpu().numpy(), L) and np.array_equal(dr.cpu().numpy(), R)
+
+
+def test_rejects_absorption_and_hrtf_outside_unit_interval():
+    """The int64 fixed-point histogram's headroom needs energies that never grow: absorption in
+    [0, 1] (or the receiver marks -1 / -2) and hrtf_absorption_rate in [0, 1]."""
+    from audiorenderingv2_amd import ArxError
+
+    tv = np.zeros((2, 9), np.float32)
+    tv[:, 3] = 1.0
+    tv[:, 7] = 1.0
+    r = AudioRenderer(RenderSettings(rays=(4, 4, 4), sample_rate=16000))
+    for bad in (1.5, -0.25, float("nan")):
+        with pytest.raises(ArxError):
+            r.set_scene(Scene(tv, np.array([0.5, bad], np.float32), []))
+    r.set_scene(Scene(tv, np.array([0.0, 1.0], np.float32), []))
+    with pytest.raises(ArxError):
+        r.set_hrtf_absorption_rate(1.25)
