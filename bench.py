@@ -19,6 +19,7 @@ count, devicePrograms.cu:208) and convolves its own copy of the stream.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -231,6 +232,20 @@ def load_profile(name: str) -> dict | None:
     return None
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Send whatever native libraries write on fd 1 to fd 2 for the duration."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,12 +283,13 @@ def main(argv=None) -> int:
                               device=local)
     scene = conference_standin()
     receiver = receiver_local()
-    if world > 1:  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
-        uid = [RenderGroup.unique_id() if rank == 0 else None]
-        D.broadcast_object(uid)
-        g = RenderGroup.rank(settings, world, rank, uid[0], scene=scene, receiver=receiver)
-    else:
-        g = RenderGroup(settings, devices=[local], scene=scene, receiver=receiver)
+    with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
+        if world > 1:  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
+            uid = [RenderGroup.unique_id() if rank == 0 else None]
+            D.broadcast_object(uid)
+            g = RenderGroup.rank(settings, world, rank, uid[0], scene=scene, receiver=receiver)
+        else:
+            g = RenderGroup(settings, devices=[local], scene=scene, receiver=receiver)
     g.setEmitterPosInOptix(CONFERENCE_EMITTER)
     g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
     m = g.member(0)
