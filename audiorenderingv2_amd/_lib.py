@@ -112,6 +112,7 @@ SIGNATURES = {
     "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
     "arx_convolute_live_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "arx_prepare_ir_spectra": (C.c_int, [_P, C.c_int]),
+    "arx_conv_describe": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_size_t]),
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),

@@ -839,6 +839,16 @@ arx_status arx_prepare_ir_spectra(arx_renderer* r, int which) {
     return st;
 }
 
+arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len) {
+    if (!r || !buf || len == 0) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL renderer or buffer");
+    if (which != 1 && which != 2) return fail(ARX_ERR_INVALID_ARGUMENT, "which must be 1 (file) or 2 (live)");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = which == 1 ? ensure_conv(r) : ensure_conv_live(r, 1);
+    if (st != ARX_OK) return st;
+    std::snprintf(buf, len, "%s", conv_plan_describe(which == 1 ? r->conv : r->conv_live));
+    return ARX_OK;
+}
+
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
                                 float* d_out_right) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");

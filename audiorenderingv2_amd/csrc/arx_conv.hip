@@ -18,8 +18,12 @@
 //   C  inverse column FFTs -> M * linear convolution of each block, to a f64 scratch;
 //   D  overlap-add gather with the circular fold cc[i] = lin[i] + lin[i+n], scaled
 //      n/(M*(n/2)), rounded once to f32 (deterministic, no atomics).
-// The FFT length M is the power of two >= n + sr - 1 (linear convolution, then folded
-// back to length n), so every (ir_len, sr) pair works with radix-4/2 Stockham stages.
+// FFT length: when n = N1 x N2 with both factors 7-smooth and <= 512 (every 2-s IR at the usual
+// rates: 96000 = 300 x 320 at 48 kHz), M = n itself -- the reference's own circular length -- with
+// mixed-radix (8/4/2/3/5/7) sub-FFTs and no fold ("direct" path, pass_*_mr).  Otherwise M is the
+// power of two >= n + sr - 1 (linear convolution, folded back to length n in pass D), so every
+// (ir_len, sr) pair works with radix-8/4/2 stages.  At C3 the direct path moves 2.7x fewer
+// FFT points per block pair than 2^18.
 // All FFT arithmetic is f64: the result matches the f64 oracle to ~1e-15 relative
 // before the single f32 rounding (the "1 ULP of max|y|" bar of SURVEY.md §8c).
 #include <hip/hip_runtime.h>
@@ -34,10 +38,21 @@
 
 namespace arx {
 
+constexpr int kMaxRadices = 12;
+constexpr int kMaxSubLen = 512;  // N1, N2 <= 512: n <= 2^18 (longer IRs take the power-of-two path)
+
+struct Factors {
+    int32_t L;
+    int32_t count;
+    int32_t r[kMaxRadices];
+};
+
 struct ConvPlan {
+    bool direct = false;  // mixed-radix FFTs of length n (no fold); else the power-of-two path
+    Factors f1{}, f2{};   // direct: the radices of N1 and N2
     int32_t n = 0;      // ir_len (circular length of the reference)
     int32_t sr = 0;     // hop (block length)
-    int32_t M = 0;      // FFT length (power of two)
+    int32_t M = 0;      // FFT length (power of two >= n + sr - 1, or n on the direct path)
     int32_t N1 = 0, N2 = 0, lg1 = 0, lg2 = 0;
     int32_t tc = 1;     // columns per workgroup in passes A / C
     int device = 0;
@@ -504,10 +519,389 @@ __global__ __launch_bounds__(kThreads) void pass_d_live(PassArgs a) {
     }
 }
 
+// ==================================================================================================
+// Mixed-radix direct path: when ir_len n = N1 x N2 with both factors 7-smooth and <= 1024 (every
+// 2 s IR at 16 / 32 / 44.1 / 48 / 96 kHz), the block circular convolution of length n is computed
+// with FFTs of length n itself -- the reference's own transform length (cuFFT, kernels.cu:413-437)
+// -- instead of the power of two >= n + sr - 1 and the fold: 96000 instead of 2^18 points per
+// 48 kHz block pair, no fold terms in pass D.  Same four passes and layouts as above; the sub-FFTs
+// are one wave per row / column in LDS, Stockham stages of radix 8, 4, 2, 3, 5, 7.
+
+// y[q] = sum_r x[r] e^(sign 2 pi i r q / R) for odd prime R, with the cos / sin of 2 pi m / R
+template <int R>
+struct OddDft;
+template <>
+struct OddDft<3> {
+    static constexpr double c[3] = {1.0, -0.5, -0.5};
+    static constexpr double s[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+};
+template <>
+struct OddDft<5> {
+    static constexpr double c[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410, -0.80901699437494742410,
+                                    0.30901699437494742410};
+    static constexpr double s[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917, -0.58778525229247312917,
+                                    -0.95105651629515357212};
+};
+template <>
+struct OddDft<7> {
+    static constexpr double c[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
+                                    -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
+    static constexpr double s[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
+                                    -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
+};
+
+template <int R>
+__device__ __forceinline__ void dft_radix(double2* x, int sign) {
+    if constexpr (R == 2) {
+        const double2 a = x[0], b = x[1];
+        x[0] = cadd(a, b);
+        x[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        dft4(x, sign);
+    } else if constexpr (R == 8) {
+        dft8(x, sign);
+    } else {  // odd prime: pair r with R - r
+        constexpr int H = R / 2;
+        double2 a[H + 1], b[H + 1];
+#pragma unroll
+        for (int r = 1; r <= H; ++r) {
+            a[r] = cadd(x[r], x[R - r]);
+            b[r] = csub(x[r], x[R - r]);
+        }
+        double2 y0 = x[0];
+#pragma unroll
+        for (int r = 1; r <= H; ++r) y0 = cadd(y0, a[r]);
+        double2 y[R];
+#pragma unroll
+        for (int q = 1; q <= H; ++q) {
+            double2 t = x[0], u = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int r = 1; r <= H; ++r) {
+                const int m = (r * q) % R;
+                t.x += OddDft<R>::c[m] * a[r].x;
+                t.y += OddDft<R>::c[m] * a[r].y;
+                u.x += OddDft<R>::s[m] * b[r].x;
+                u.y += OddDft<R>::s[m] * b[r].y;
+            }
+            const double2 iu = mul_si(u, sign);  // sign * i * u
+            y[q] = cadd(t, iu);
+            y[R - q] = csub(t, iu);
+        }
+        x[0] = y0;
+#pragma unroll
+        for (int q = 1; q < R; ++q) x[q] = y[q];
+    }
+}
+
+// One Stockham stage of radix R over buf[0..L) (LDS, this wave's row / column), Ns = product of
+// the earlier radices; twl = W_L^e.  Every lane first reads all its butterflies, then writes.
+template <int R>
+__device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L, int Ns, int j, int sign) {
+    constexpr int kMaxB = (kMaxSubLen / R + 63) / 64;
+    const int nb = L / R, step = L / (Ns * R);
+    double2 v[kMaxB][R];
+#pragma unroll
+    for (int i = 0; i < kMaxB; ++i) {
+        const int b = j + 64 * i;
+        if (b < nb) {
+            const int k = b % Ns;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                double2 x = buf[b + q * nb];
+                if (q > 0) {
+                    const double2 w = twl[q * k * step];
+                    x = cmul(x, sign < 0 ? w : make_double2(w.x, -w.y));
+                }
+                v[i][q] = x;
+            }
+            dft_radix<R>(v[i], sign);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < kMaxB; ++i) {
+        const int b = j + 64 * i;
+        if (b < nb) {
+            const int k = b % Ns;
+            const int d = (b - k) * R + k;
+#pragma unroll
+            for (int q = 0; q < R; ++q) buf[d + q * Ns] = v[i][q];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// In-place FFT of buf[0..f.L) by one wave (lane j), natural order in and out.
+__device__ __forceinline__ void fft_mr_wave(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
+    int Ns = 1;
+    for (int s = 0; s < f.count; ++s) {
+        switch (f.r[s]) {
+            case 8: mr_stage<8>(buf, twl, f.L, Ns, j, sign); break;
+            case 4: mr_stage<4>(buf, twl, f.L, Ns, j, sign); break;
+            case 2: mr_stage<2>(buf, twl, f.L, Ns, j, sign); break;
+            case 3: mr_stage<3>(buf, twl, f.L, Ns, j, sign); break;
+            case 5: mr_stage<5>(buf, twl, f.L, Ns, j, sign); break;
+            default: mr_stage<7>(buf, twl, f.L, Ns, j, sign); break;
+        }
+        Ns *= f.r[s];
+    }
+}
+
+// Workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous run of tiles, so
+// that the tiles sharing a 128-B line (pass A's f32 rows, pass C's f64 rows) share its L2.
+__device__ __forceinline__ int xcd_tile(int bid, int nblk) {
+    return (nblk & 7) ? bid : (bid & 7) * (nblk >> 3) + (bid >> 3);
+}
+
+struct MrArgs {
+    PassArgs p;
+    Factors f1, f2;  // the column (N1) and row (N2) sub-FFTs
+};
+
+constexpr int kMrIt = kMaxSubLen / 64;  // per-lane elements of one row / column, and per-thread tile loads
+
+// dst[i] = src[i * stride], i < count, by the nt threads (all loads issued before the LDS stores)
+__device__ __forceinline__ void stage_table(double2* dst, const double2* __restrict__ src, int count, int stride,
+                                            int nt) {
+    double2 v[kMrIt];
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        v[it] = i < count ? src[(size_t)i * stride] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        if (i < count) dst[i] = v[it];
+    }
+}
+
+// W_n^e = W_N1^(e / N2) * W_n^(e mod N2) for e < n, from the LDS tables tq[q] = W_N1^q, tr[r] = W_n^r.
+__device__ __forceinline__ double2 tw_n(const double2* tq, const double2* tr, int e, int N2) {
+    const int q = e / N2;
+    return cmul(tq[q], tr[e - q * N2]);
+}
+
+// Pass A: forward column FFTs of length N1 (one wave per column, tc = waves per block), * W_n^(n2 k1),
+// stored transposed S[k1 N2 + n2].  LDS: tile tc x N1, W_N1 (N1), W_n^r (N2).
+template <int MODE>
+__global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const PassArgs& a = m.p;
+    const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
+    const int64_t batch = blockIdx.y;
+    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
+    double2* twl = lds + (size_t)tc * N1;
+    double2* tr = twl + N1;
+    double2 v[kMrIt];
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {  // every load in flight before the first use
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
+        const int64_t idx = (int64_t)N2 * n1 + n2;
+        double2 x = make_double2(0.0, 0.0);
+        if (n1 < N1 && n2 < N2) {
+            if (MODE == 0) {
+                if (idx < a.sr) {
+                    const int64_t b0 = 2 * batch, b1 = 2 * batch + 1;
+                    if (b0 < a.n_blocks) x.x = (double)a.in[b0 * a.sr + idx];
+                    if (b1 < a.n_blocks) x.y = (double)a.in[b1 * a.sr + idx];
+                }
+            } else if (MODE == 2) {
+                if (idx < a.n_in) x.x = a.in_d[idx];
+            } else {
+                x.x = (double)(batch == 0 ? a.ir_l : a.ir_r)[idx];
+            }
+        }
+        v[it] = x;
+    }
+    stage_table(twl, a.tw, N1, N2, nt);  // W_N1^i = W_n^(i N2)
+    stage_table(tr, a.tw, N2, 1, nt);
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), n1 = i >> lgc;
+        if (n1 < N1) lds[(size_t)c * N1 + n1] = v[it];
+    }
+    __syncthreads();
+    fft_mr_wave(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
+    __syncthreads();
+    double2* dst = (MODE != 1) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), k1 = i >> lgc, n2 = n2_0 + c;
+        if (k1 < N1 && n2 < N2)
+            dst[(int64_t)k1 * N2 + n2] = cmul(lds[(size_t)c * N1 + k1], tw_n(twl, tr, n2 * k1, N2));
+    }
+}
+
+// Pass B: per row k1 (one wave; nt / 64 rows per block): forward row FFT (N2); mode 1 stores it (IR
+// spectrum); mode 0 multiplies by H_c, inverse row FFT, * W_n^(-n2 k1), for both channels.
+// LDS: 2 x N2 per row, W_N2 (N2), W_N1 (N1), W_n^r (N2).
+template <int MODE>
+__global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const PassArgs& a = m.p;
+    const int nt = blockDim.x, rows = nt >> 6, N1 = a.N1, N2 = a.N2;
+    const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+    const int k1 = blockIdx.x * rows + w;
+    const int64_t batch = blockIdx.y;
+    double2* spec = lds + (size_t)w * 2 * N2;
+    double2* work = spec + N2;
+    double2* tw2 = lds + (size_t)rows * 2 * N2;
+    double2* tq = tw2 + N2;
+    double2* tr = tq + N1;
+    const bool live = k1 < N1;
+    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
+    double2 v[kMrIt], h[kMrIt];
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = j + 64 * it;
+        const bool in = live && i < N2;
+        v[it] = in ? row[i] : make_double2(0.0, 0.0);
+        h[it] = (MODE == 0 && in) ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);  // H_0's row
+    }
+    stage_table(tw2, a.tw, N2, N1, nt);  // W_N2^i = W_n^(i N1)
+    if (MODE == 0) {
+        stage_table(tq, a.tw, N1, N2, nt);
+        stage_table(tr, a.tw, N2, 1, nt);
+    }
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = j + 64 * it;
+        if (live && i < N2) spec[i] = v[it];
+    }
+    __syncthreads();
+    if (!live) return;  // no block barrier below
+    fft_mr_wave(spec, tw2, m.f2, j, -1);
+    if (MODE == 1) {
+#pragma unroll
+        for (int it = 0; it < kMrIt; ++it) {
+            const int i = j + 64 * it;
+            if (i < N2) row[i] = spec[i];
+        }
+        return;
+    }
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int it = 0; it < kMrIt; ++it) {
+            const int i = j + 64 * it;
+            if (i < N2) work[i] = cmul(spec[i], h[it]);
+        }
+        if (c == 0) {  // H_1's row, in flight during the inverse FFT
+#pragma unroll
+            for (int it = 0; it < kMrIt; ++it) {
+                const int i = j + 64 * it;
+                h[it] = i < N2 ? a.H[(size_t)a.M + (int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        fft_mr_wave(work, tw2, m.f2, j, +1);
+        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
+#pragma unroll
+        for (int it = 0; it < kMrIt; ++it) {
+            const int i = j + 64 * it;
+            if (i < N2) {
+                const double2 t = tw_n(tq, tr, i * k1, N2);
+                dst[i] = cmul(work[i], make_double2(t.x, -t.y));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
+// blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x N1, W_N1 (N1).
+__global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const PassArgs& a = m.p;
+    const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
+    const int64_t pair = blockIdx.y >> 1;
+    const int ch = blockIdx.y & 1;
+    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
+    const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
+    double2* twl = lds + (size_t)tc * N1;
+    double2 v[kMrIt];
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), k1 = i >> lgc, n2 = n2_0 + c;
+        v[it] = (k1 < N1 && n2 < N2) ? src[(int64_t)k1 * N2 + n2] : make_double2(0.0, 0.0);
+    }
+    stage_table(twl, a.tw, N1, N2, nt);
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), k1 = i >> lgc;
+        if (k1 < N1) lds[(size_t)c * N1 + k1] = v[it];
+    }
+    __syncthreads();
+    fft_mr_wave(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
+    __syncthreads();
+    const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
+    double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
+    double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
+#pragma unroll
+    for (int it = 0; it < kMrIt; ++it) {
+        const int i = threadIdx.x + it * nt;
+        const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
+        if (n1 < N1 && n2 < N2) {
+            const int64_t idx = (int64_t)N2 * n1 + n2;
+            const double2 x = lds[(size_t)c * N1 + n1];
+            if (b0 < a.n_blocks) y0[idx] = x.x;
+            if (b1 < a.n_blocks) y1[idx] = x.y;
+        }
+    }
+}
+
 int ilog2(int64_t v) {
     int l = 0;
     while (((int64_t)1 << l) < v) ++l;
     return l;
+}
+
+// L = 8^a 4^b 2^c 3^d 5^e 7^f; false if L has another prime factor
+bool factor7(int32_t L, Factors& f) {
+    f.L = L;
+    f.count = 0;
+    int32_t v = L, twos = 0;
+    while (v % 2 == 0) {
+        v /= 2;
+        ++twos;
+    }
+    auto push = [&](int r) {
+        if (f.count < kMaxRadices) f.r[f.count] = r;
+        ++f.count;
+    };
+    for (; twos >= 3; twos -= 3) push(8);
+    if (twos == 2) push(4);
+    if (twos == 1) push(2);
+    for (int q : {3, 5, 7})
+        while (v % q == 0) {
+            v /= q;
+            push(q);
+        }
+    return v == 1 && f.count <= kMaxRadices;
+}
+
+// n = N1 x N2, both 7-smooth and <= kMaxSubLen; prefer N2 % 8 == 0 (full 128-B row segments in
+// passes A / C), then the most balanced split.
+bool direct_split(int32_t n, int32_t& N1, int32_t& N2) {
+    Factors f;
+    int64_t best = -1;
+    for (int32_t d = 2; d <= kMaxSubLen; ++d) {
+        if (n % d) continue;
+        const int32_t e = n / d;
+        if (e < 2 || e > kMaxSubLen || !factor7(d, f) || !factor7(e, f)) continue;
+        const int64_t score = (e % 8 ? 1000000 : 0) + std::abs(d - e);
+        if (best < 0 || score < best) {
+            best = score;
+            N1 = d;
+            N2 = e;
+        }
+    }
+    return best >= 0;
 }
 
 }  // namespace
@@ -524,15 +918,26 @@ ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char
     ConvPlan* p = new ConvPlan();
     p->n = ir_len;
     p->sr = sample_rate;
-    p->M = 1 << lg;
-    p->lg1 = lg / 2;
-    p->lg2 = lg - p->lg1;
-    p->N1 = 1 << p->lg1;
-    p->N2 = 1 << p->lg2;
-    p->tc = std::max(1, std::min(std::min(16, p->N2), 4096 / p->N1));
     p->device = device;
-    std::snprintf(p->desc, sizeof(p->desc), "pow2 linear+fold: n=%d sr=%d M=%d (%dx%d) f64", p->n, p->sr, p->M, p->N1,
-                  p->N2);
+    int32_t d1 = 0, d2 = 0;
+    if (ir_len >= sample_rate && direct_split(ir_len, d1, d2) && factor7(d1, p->f1) && factor7(d2, p->f2)) {
+        p->direct = true;
+        p->M = ir_len;
+        p->N1 = d1;
+        p->N2 = d2;
+        p->tc = 8;  // unused on this path (see mr_tiles)
+        std::snprintf(p->desc, sizeof(p->desc), "mixed-radix direct circular: n=%d sr=%d (%dx%d) f64", p->n, p->sr,
+                      p->N1, p->N2);
+    } else {
+        p->M = 1 << lg;
+        p->lg1 = lg / 2;
+        p->lg2 = lg - p->lg1;
+        p->N1 = 1 << p->lg1;
+        p->N2 = 1 << p->lg2;
+        p->tc = std::max(1, std::min(std::min(16, p->N2), 4096 / p->N1));
+        std::snprintf(p->desc, sizeof(p->desc), "pow2 linear+fold: n=%d sr=%d M=%d (%dx%d) f64", p->n, p->sr, p->M,
+                      p->N1, p->N2);
+    }
     hipSetDevice(device);
     std::vector<double2> tw((size_t)p->M);
     const long double two_pi = 6.283185307179586476925286766559L;
@@ -571,6 +976,11 @@ static void launch_pass_b(const ConvPlan* p, unsigned batches, const PassArgs& a
         hipLaunchKernelGGL(pass_b<MODE>, dim3(p->N1, batches), dim3(kThreads), 2 * (size_t)p->N2 * sizeof(double2), s, a);
 }
 
+// per block and channel: n (direct) or the linear length n + sr - 1 that pass D folds
+static int64_t plan_ylen(const ConvPlan* p) {
+    return p->direct ? (int64_t)p->n : (int64_t)p->n + std::min(p->n, p->sr) - 1;
+}
+
 static PassArgs base_args(const ConvPlan* p) {
     PassArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -584,8 +994,26 @@ static PassArgs base_args(const ConvPlan* p) {
     a.n = p->n;
     a.sr = p->sr;
     a.H = p->d_H;
-    a.ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    a.ylen = plan_ylen(p);
     return a;
+}
+
+static MrArgs mr_args(const ConvPlan* p, const PassArgs& a) {
+    MrArgs m;
+    m.p = a;
+    m.f1 = p->f1;
+    m.f2 = p->f2;
+    return m;
+}
+// Direct-path launch shapes: passes A / C run one wave per column, tc columns per block (8 for the
+// batched block pairs, 2 for the two IR channels and the single live block, for more blocks);
+// pass B one wave per row, `rows` rows per block.
+static unsigned mr_tiles(const ConvPlan* p, int tc) { return (unsigned)((p->N2 + tc - 1) / tc); }
+static size_t mr_lds_a(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1 + p->N2) * sizeof(double2); }
+static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1) * sizeof(double2); }
+static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
+static size_t mr_lds_b(const ConvPlan* p, int rows) {
+    return ((size_t)rows * 2 * p->N2 + 2 * p->N2 + p->N1) * sizeof(double2);
 }
 
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
@@ -594,6 +1022,12 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     a.ir_l = d_ir_left;
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
+    if (p->direct) {
+        const MrArgs m = mr_args(p, a);
+        hipLaunchKernelGGL(pass_a_mr<1>, dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
+        hipLaunchKernelGGL(pass_b_mr<1>, dim3(mr_rows(p, 1), 2), dim3(64), mr_lds_b(p, 1), s, m);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
     launch_pass_b<1>(p, 2, a, s);
     return hipGetLastError();
@@ -609,7 +1043,7 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
         return e;
     }
     const int64_t pairs = (S + 1) / 2;
-    const int64_t ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    const int64_t ylen = plan_ylen(p);
     if (pairs > p->pairs_cap) {
         hipFree(p->d_S);
         hipFree(p->d_Y);
@@ -634,9 +1068,16 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.out_r = d_out_right;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
-    hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
-    launch_pass_b<0>(p, (unsigned)pairs, a, s);
-    hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
+    if (p->direct) {
+        const MrArgs m = mr_args(p, a);
+        hipLaunchKernelGGL(pass_a_mr<0>, dim3(mr_tiles(p, 8), (unsigned)pairs), dim3(512), mr_lds_a(p, 8), s, m);
+        hipLaunchKernelGGL(pass_b_mr<0>, dim3(mr_rows(p, 4), (unsigned)pairs), dim3(256), mr_lds_b(p, 4), s, m);
+        hipLaunchKernelGGL(pass_c_mr, dim3(mr_tiles(p, 8), (unsigned)(2 * pairs)), dim3(512), mr_lds_c(p, 8), s, m);
+    } else {
+        hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
+        launch_pass_b<0>(p, (unsigned)pairs, a, s);
+        hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
+    }
     hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
@@ -645,7 +1086,7 @@ int32_t conv_plan_block(const ConvPlan* p) { return p ? p->sr : 0; }
 
 hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s) {
     if (n_in < 0 || n_in > p->sr) return hipErrorInvalidValue;
-    const int64_t ylen = (int64_t)p->n + std::min(p->n, p->sr) - 1;
+    const int64_t ylen = plan_ylen(p);
     if (p->pairs_cap < 1) {
         hipFree(p->d_S);
         hipFree(p->d_Y);
@@ -668,9 +1109,16 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.out_d = d_out_interleaved;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
-    hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
-    launch_pass_b<0>(p, 1, a, s);
-    hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
+    if (p->direct) {
+        const MrArgs m = mr_args(p, a);
+        hipLaunchKernelGGL(pass_a_mr<2>, dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
+        hipLaunchKernelGGL(pass_b_mr<0>, dim3(mr_rows(p, 1), 1), dim3(64), mr_lds_b(p, 1), s, m);
+        hipLaunchKernelGGL(pass_c_mr, dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
+    } else {
+        hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
+        launch_pass_b<0>(p, 1, a, s);
+        hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
+    }
     hipLaunchKernelGGL(pass_d_live, dim3((unsigned)((p->n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }

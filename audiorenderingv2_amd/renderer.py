@@ -248,6 +248,12 @@ class AudioRenderer:
         """Recompute the cached IR spectra now (async) rather than in the next convolution."""
         check(lib().arx_prepare_ir_spectra(self._h, (1 if file else 0) | (2 if live else 0)))
 
+    def conv_plan(self, live: bool = False) -> str:
+        """The convolution plan in use (arx_conv_describe): direct mixed-radix or power-of-two."""
+        buf = C.create_string_buffer(256)
+        check(lib().arx_conv_describe(self._h, 2 if live else 1, buf, len(buf)))
+        return buf.value.decode()
+
     def convolute_live_device(self, d_in: int, n_in: int, d_out: int) -> None:
         check(lib().arx_convolute_live_device(self._h, C.c_void_p(d_in), n_in, C.c_void_p(d_out)))
 

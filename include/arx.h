@@ -212,6 +212,11 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
  * next convolution: which = 1 file path, 2 live path, 3 both.  Lets a moving-listener frame
  * (re-trace + reduce + new spectra) finish before audio needs it. */
 arx_status arx_prepare_ir_spectra(arx_renderer* r, int which);
+/* Describe the convolution plan (which = 1 file path, 2 live path; created if needed) into
+ * buf[len]: "mixed-radix direct circular: n=.. sr=.. (N1xN2) f64" when ir_len factors into two
+ * 7-smooth sub-lengths <= 512 (FFT length = ir_len, as the reference's cuFFT plans), else
+ * "pow2 linear+fold: ..." (power-of-two length >= ir_len + block - 1, folded back). */
+arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len);
 
 /* Streaming convolution for the RtAudio duplex callback (replaces the
  * per-callback full-length circular convolution of convoluteLiveInput, AudioRenderer.cpp:593-661,

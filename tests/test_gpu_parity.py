@@ -335,7 +335,8 @@ def sparse_ir(n, rng, k=300, scale=1e-4):
 
 @pytest.mark.parametrize("sr,secs,length", [(1000, 2, 10555), (1000, 2, 999), (1000, 2, 4000), (800, 3, 7777),
                                             (16000, 2, 128000), (441, 2, 5000), (32000, 2, 70000),
-                                            (22050, 1, 50000), (44100, 2, 100000)])
+                                            (22050, 1, 50000), (44100, 2, 100000), (1125, 2, 9000),
+                                            (1100, 2, 6000), (48000, 1, 100000)])
 def test_convolution_matches_oracle(sr, secs, length):
     rng = np.random.default_rng(sr + length)
     n = sr * secs
@@ -350,6 +351,20 @@ def test_convolution_matches_oracle(sr, secs, length):
             assert not got.any()
         else:
             assert np.abs(got - ref).max() <= ulp_of_max(ref)
+
+
+@pytest.mark.parametrize("sr,secs,live,expect", [
+    (48000, 2, False, "mixed-radix direct circular: n=96000 sr=48000 (300x320)"),  # C3
+    (16000, 2, False, "mixed-radix direct circular: n=32000 sr=16000 (160x200)"),  # C1 / C2
+    (44100, 2, True, "mixed-radix direct circular: n=88200 sr=4096 (315x280)"),    # the mic path
+    (1125, 2, False, "mixed-radix direct circular: n=2250 sr=1125"),               # ragged column tiles
+    (1100, 2, False, "pow2 linear+fold: n=2200 sr=1100 M=4096"),                    # 11 | n
+])
+def test_convolution_plan_choice(sr, secs, live, expect):
+    """FFT length = ir_len (the reference's own cuFFT length) whenever ir_len = N1 x N2 with 7-smooth
+    factors <= 512; the power-of-two linear convolution + fold otherwise.  Both are checked
+    against the oracle above."""
+    assert conv_renderer(sr, secs).conv_plan(live=live).startswith(expect)
 
 
 def test_convolution_c3_size_with_rendered_ir(conference):
