@@ -799,14 +799,16 @@ arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right
     return ARX_OK;
 }
 
-static arx_status ensure_conv(arx_renderer* r) {
+// spectra = false: leave a changed IR's spectra to the next conv_run (which folds them into its
+// own first pass)
+static arx_status ensure_conv(arx_renderer* r, bool spectra = true) {
     if (!r->conv) {
         char err[256] = {0};
         r->conv = conv_plan_create(r->ir_len, r->cfg.sample_rate, r->cfg.device, err, sizeof(err));
         if (!r->conv) return fail(ARX_ERR_INTERNAL, "convolution plan: %s", err);
         r->conv_ir_dirty = true;
     }
-    if (r->conv_ir_dirty) {
+    if (spectra && r->conv_ir_dirty) {
         ARX_HIP(conv_set_ir(r->conv, r->d_ir, r->d_ir + r->ir_len, r->stream));
         r->conv_ir_dirty = false;
     }
@@ -854,10 +856,13 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (n_frames > 0 && (!d_in || !d_out_left || !d_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    arx_status st = ensure_conv(r);
+    arx_status st = ensure_conv(r, false);
     if (st != ARX_OK) return st;
+    const bool ir_new = r->conv_ir_dirty;
     ARX_HIP(hipEventRecord(r->cev0, r->stream));
-    ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, r->stream));
+    ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
+                     ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
+    r->conv_ir_dirty = false;
     ARX_HIP(hipEventRecord(r->cev1, r->stream));
     ++r->conv_launches;
     return ARX_OK;

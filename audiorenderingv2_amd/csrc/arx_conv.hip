@@ -49,6 +49,7 @@ struct Factors {
 
 struct ConvPlan {
     bool direct = false;  // mixed-radix FFTs of length n (no fold); else the power-of-two path
+    bool r7 = false;      // direct: radix-7 stages present (selects the kernels that carry them)
     Factors f1{}, f2{};   // direct: the radices of N1 and N2
     int32_t n = 0;      // ir_len (circular length of the reference)
     int32_t sr = 0;     // hop (block length)
@@ -631,7 +632,9 @@ __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L
     __builtin_amdgcn_wave_barrier();
 }
 
-// In-place FFT of buf[0..f.L) by one wave (lane j), natural order in and out.
+// In-place FFT of buf[0..f.L) by one wave (lane j), natural order in and out.  R7: the plan has
+// radix-7 stages (their 7-point DFT costs ~20 VGPRs in every kernel that may run one).
+template <bool R7>
 __device__ __forceinline__ void fft_mr_wave(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
     int Ns = 1;
     for (int s = 0; s < f.count; ++s) {
@@ -641,7 +644,9 @@ __device__ __forceinline__ void fft_mr_wave(double2* buf, const double2* twl, co
             case 2: mr_stage<2>(buf, twl, f.L, Ns, j, sign); break;
             case 3: mr_stage<3>(buf, twl, f.L, Ns, j, sign); break;
             case 5: mr_stage<5>(buf, twl, f.L, Ns, j, sign); break;
-            default: mr_stage<7>(buf, twl, f.L, Ns, j, sign); break;
+            default:
+                if constexpr (R7) mr_stage<7>(buf, twl, f.L, Ns, j, sign);
+                break;
         }
         Ns *= f.r[s];
     }
@@ -656,6 +661,8 @@ __device__ __forceinline__ int xcd_tile(int bid, int nblk) {
 struct MrArgs {
     PassArgs p;
     Factors f1, f2;  // the column (N1) and row (N2) sub-FFTs
+    int32_t batches;  // pass B: batches in its 1-D grid
+    int32_t fuse2;    // pass C: n == 2 sr and N1 even -- write the pair's odd output segment directly
 };
 
 constexpr int kMrIt = kMaxSubLen / 64;  // per-lane elements of one row / column, and per-thread tile loads
@@ -683,13 +690,17 @@ __device__ __forceinline__ double2 tw_n(const double2* tq, const double2* tr, in
 }
 
 // Pass A: forward column FFTs of length N1 (one wave per column, tc = waves per block), * W_n^(n2 k1),
-// stored transposed S[k1 N2 + n2].  LDS: tile tc x N1, W_N1 (N1), W_n^r (N2).
-template <int MODE>
+// stored transposed S[k1 N2 + n2].  LDS: tile tc x N1, W_N1 (N1), W_n^r (N2).  Mode 0 batches past
+// the block pairs (batch = n_pairs + c) are the IR channels c: their columns go to H, so the IR
+// spectra's column pass rides in the same launch as the audio's.
+template <int MODE, bool R7>
 __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
     const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
     const int64_t batch = blockIdx.y;
+    const bool ir = MODE == 1 || (MODE == 0 && batch >= a.n_pairs);
+    const int64_t ch = MODE == 1 ? batch : batch - a.n_pairs;
     const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
     double2* twl = lds + (size_t)tc * N1;
     double2* tr = twl + N1;
@@ -701,16 +712,16 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
         const int64_t idx = (int64_t)N2 * n1 + n2;
         double2 x = make_double2(0.0, 0.0);
         if (n1 < N1 && n2 < N2) {
-            if (MODE == 0) {
+            if (ir) {
+                x.x = (double)(ch == 0 ? a.ir_l : a.ir_r)[idx];
+            } else if (MODE == 0) {
                 if (idx < a.sr) {
                     const int64_t b0 = 2 * batch, b1 = 2 * batch + 1;
                     if (b0 < a.n_blocks) x.x = (double)a.in[b0 * a.sr + idx];
                     if (b1 < a.n_blocks) x.y = (double)a.in[b1 * a.sr + idx];
                 }
-            } else if (MODE == 2) {
-                if (idx < a.n_in) x.x = a.in_d[idx];
             } else {
-                x.x = (double)(batch == 0 ? a.ir_l : a.ir_r)[idx];
+                if (idx < a.n_in) x.x = a.in_d[idx];
             }
         }
         v[it] = x;
@@ -724,9 +735,9 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
         if (n1 < N1) lds[(size_t)c * N1 + n1] = v[it];
     }
     __syncthreads();
-    fft_mr_wave(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
+    fft_mr_wave<R7>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
-    double2* dst = (MODE != 1) ? a.S + (size_t)batch * 3 * a.M : a.H + (size_t)batch * a.M;
+    double2* dst = ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
 #pragma unroll
     for (int it = 0; it < kMrIt; ++it) {
         const int i = threadIdx.x + it * nt;
@@ -738,20 +749,24 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
 
 // Pass B: per row k1 (one wave; nt / 64 rows per block): forward row FFT (N2); mode 1 stores it (IR
 // spectrum); mode 0 multiplies by H_c, inverse row FFT, * W_n^(-n2 k1), for both channels.
-// LDS: 2 x N2 per row, W_N2 (N2), W_N1 (N1), W_n^r (N2).
-template <int MODE>
+// LDS: 2 x N2 per row (the spectrum; H_0's row, then the product), W_N2 (N2) -- small enough for
+// 3 blocks per CU, so one round of blocks covers the C3 grid.
+template <int MODE, bool R7>
 __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
     const int nt = blockDim.x, rows = nt >> 6, N1 = a.N1, N2 = a.N2;
     const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
-    const int k1 = blockIdx.x * rows + w;
-    const int64_t batch = blockIdx.y;
+    // 1-D grid of (row group, batch), dealt so that every batch of a row group runs on the same XCD:
+    // the H rows the batches share are fetched into that XCD's L2 once, not once per batch.
+    const int batches = (int)m.batches;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int group = (slot / batches) * 8 + xcd;
+    const int64_t batch = slot % batches;
+    const int k1 = group * rows + w;
     double2* spec = lds + (size_t)w * 2 * N2;
     double2* work = spec + N2;
     double2* tw2 = lds + (size_t)rows * 2 * N2;
-    double2* tq = tw2 + N2;
-    double2* tr = tq + N1;
     const bool live = k1 < N1;
     double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
     double2 v[kMrIt], h[kMrIt];
@@ -763,18 +778,17 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
         h[it] = (MODE == 0 && in) ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);  // H_0's row
     }
     stage_table(tw2, a.tw, N2, N1, nt);  // W_N2^i = W_n^(i N1)
-    if (MODE == 0) {
-        stage_table(tq, a.tw, N1, N2, nt);
-        stage_table(tr, a.tw, N2, 1, nt);
-    }
 #pragma unroll
     for (int it = 0; it < kMrIt; ++it) {
         const int i = j + 64 * it;
-        if (live && i < N2) spec[i] = v[it];
+        if (live && i < N2) {
+            spec[i] = v[it];
+            if (MODE == 0) work[i] = h[it];
+        }
     }
     __syncthreads();
     if (!live) return;  // no block barrier below
-    fft_mr_wave(spec, tw2, m.f2, j, -1);
+    fft_mr_wave<R7>(spec, tw2, m.f2, j, -1);
     if (MODE == 1) {
 #pragma unroll
         for (int it = 0; it < kMrIt; ++it) {
@@ -784,26 +798,20 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
         return;
     }
     for (int c = 0; c < 2; ++c) {
+        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * N2;
 #pragma unroll
         for (int it = 0; it < kMrIt; ++it) {
             const int i = j + 64 * it;
-            if (i < N2) work[i] = cmul(spec[i], h[it]);
-        }
-        if (c == 0) {  // H_1's row, in flight during the inverse FFT
-#pragma unroll
-            for (int it = 0; it < kMrIt; ++it) {
-                const int i = j + 64 * it;
-                h[it] = i < N2 ? a.H[(size_t)a.M + (int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
-            }
+            if (i < N2) work[i] = cmul(spec[i], c == 0 ? work[i] : Hc[i]);
         }
         __builtin_amdgcn_wave_barrier();
-        fft_mr_wave(work, tw2, m.f2, j, +1);
+        fft_mr_wave<R7>(work, tw2, m.f2, j, +1);
         double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
 #pragma unroll
         for (int it = 0; it < kMrIt; ++it) {
             const int i = j + 64 * it;
             if (i < N2) {
-                const double2 t = tw_n(tq, tr, i * k1, N2);
+                const double2 t = a.tw[(int64_t)i * k1];  // W_n^(n2 k1), n2 k1 < n
                 dst[i] = cmul(work[i], make_double2(t.x, -t.y));
             }
         }
@@ -813,6 +821,7 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
 
 // Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
 // blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x N1, W_N1 (N1).
+template <bool R7>
 __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
@@ -837,9 +846,40 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
         if (k1 < N1) lds[(size_t)c * N1 + k1] = v[it];
     }
     __syncthreads();
-    fft_mr_wave(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
+    fft_mr_wave<R7>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
     __syncthreads();
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
+    if (m.fuse2) {
+        // n = 2 sr, N1 even: rows n1 < N1/2 hold the first half of each block's window (i = idx < sr),
+        // rows n1 + N1/2 the second.  Output segment 2p+1 = y_2p[i + sr] + y_2p+1[i] lies inside this
+        // pair: it is written here, summed in pass D's order and rounded once.  Segment 2p needs
+        // y_2p[i] (E_p) and the previous pair's y_2p-1[i + sr] (F_p-1): pass_d2.
+        const int half = N1 >> 1;
+        const int64_t sr = a.sr;
+        float* out = ch == 0 ? a.out_l : a.out_r;
+        double* E = a.Y + (pair * 2 + ch) * 2 * sr;
+        double* F = E + sr;
+#pragma unroll
+        for (int it = 0; it < kMrIt; ++it) {
+            const int i = threadIdx.x + it * nt;
+            const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
+            if (n1 < half && n2 < N2) {
+                const int64_t idx = (int64_t)N2 * n1 + n2;
+                const double2 lo = lds[(size_t)c * N1 + n1], hi = lds[(size_t)c * N1 + n1 + half];
+                const bool odd = b1 < a.n_blocks;  // the pair's second block exists
+                const int64_t t = b1 * sr + idx;
+                if (t < a.len) {
+                    double acc = 0.0;
+                    acc += hi.x;
+                    if (odd) acc += lo.y;
+                    out[t] = (float)(acc * a.scale);
+                }
+                E[idx] = lo.x;
+                F[idx] = odd ? hi.y : 0.0;
+            }
+        }
+        return;
+    }
     double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
     double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
 #pragma unroll
@@ -853,6 +893,23 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
             if (b1 < a.n_blocks) y1[idx] = x.y;
         }
     }
+}
+
+// Pass D for the fused n = 2 sr case: the even output segments 2p = F_p-1 + E_p (pass D's order),
+// and zeros past the last window; the odd segments 2p+1 were written by pass_c_mr.
+__global__ __launch_bounds__(kThreads) void pass_d2(PassArgs a) {
+    const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= a.len) return;
+    const int ch = blockIdx.y;
+    const int64_t sr = a.sr, seg = t / sr, i = t - seg * sr;
+    if ((seg & 1) && seg < 2 * a.n_pairs) return;  // written by pass C
+    double acc = 0.0;
+    if (!(seg & 1)) {
+        const int64_t p = seg >> 1;
+        if (p >= 1 && 2 * p - 1 < a.n_blocks) acc += a.Y[((p - 1) * 2 + ch) * 2 * sr + sr + i];  // F_p-1
+        if (p < a.n_pairs) acc += a.Y[(p * 2 + ch) * 2 * sr + i];                               // E_p
+    }
+    (ch == 0 ? a.out_l : a.out_r)[t] = (float)(acc * a.scale);
 }
 
 int ilog2(int64_t v) {
@@ -922,6 +979,8 @@ ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char
     int32_t d1 = 0, d2 = 0;
     if (ir_len >= sample_rate && direct_split(ir_len, d1, d2) && factor7(d1, p->f1) && factor7(d2, p->f2)) {
         p->direct = true;
+        for (int i = 0; i < p->f1.count; ++i) p->r7 |= p->f1.r[i] == 7;
+        for (int i = 0; i < p->f2.count; ++i) p->r7 |= p->f2.r[i] == 7;
         p->M = ir_len;
         p->N1 = d1;
         p->N2 = d2;
@@ -1003,6 +1062,8 @@ static MrArgs mr_args(const ConvPlan* p, const PassArgs& a) {
     m.p = a;
     m.f1 = p->f1;
     m.f2 = p->f2;
+    m.batches = 1;
+    m.fuse2 = 0;
     return m;
 }
 // Direct-path launch shapes: passes A / C run one wave per column, tc columns per block (8 for the
@@ -1012,8 +1073,46 @@ static unsigned mr_tiles(const ConvPlan* p, int tc) { return (unsigned)((p->N2 +
 static size_t mr_lds_a(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1 + p->N2) * sizeof(double2); }
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
-static size_t mr_lds_b(const ConvPlan* p, int rows) {
-    return ((size_t)rows * 2 * p->N2 + 2 * p->N2 + p->N1) * sizeof(double2);
+static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
+template <int MODE, bool R7>
+static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipStream_t s) {
+    const unsigned groups8 = (mr_rows(p, rows) + 7) / 8 * 8;  // see pass_b_mr's XCD mapping
+    m.batches = batches;
+    hipLaunchKernelGGL((pass_b_mr<MODE, R7>), dim3(groups8 * (unsigned)batches), dim3(64 * rows), mr_lds_b(p, rows), s,
+                       m);
+}
+
+// IR spectra alone (arx_prepare_ir_spectra, the live path)
+template <bool R7>
+static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
+    const MrArgs m = mr_args(p, a);
+    hipLaunchKernelGGL((pass_a_mr<1, R7>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
+    launch_b_mr<1, R7>(p, 1, 2, m, s);
+}
+
+// File convolution; with_ir: the IR columns ride in pass A's launch as two extra batches.
+template <bool R7>
+static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
+    MrArgs m = mr_args(p, a);
+    hipLaunchKernelGGL((pass_a_mr<0, R7>), dim3(mr_tiles(p, 8), (unsigned)(pairs + (with_ir ? 2 : 0))), dim3(512),
+                       mr_lds_a(p, 8), s, m);
+    if (with_ir) launch_b_mr<1, R7>(p, 1, 2, m, s);
+    launch_b_mr<0, R7>(p, 4, (int)pairs, m, s);
+    m.fuse2 = p->n == 2 * p->sr && p->N1 % 2 == 0;
+    hipLaunchKernelGGL((pass_c_mr<R7>), dim3(mr_tiles(p, 8), (unsigned)(2 * pairs)), dim3(512), mr_lds_c(p, 8), s, m);
+    const dim3 grid_d((unsigned)((a.len + kThreads - 1) / kThreads), 2);
+    if (m.fuse2)
+        hipLaunchKernelGGL(pass_d2, grid_d, dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(pass_d, grid_d, dim3(kThreads), 0, s, a);
+}
+
+template <bool R7>
+static void mr_live(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
+    const MrArgs m = mr_args(p, a);
+    hipLaunchKernelGGL((pass_a_mr<2, R7>), dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
+    launch_b_mr<0, R7>(p, 1, 1, m, s);
+    hipLaunchKernelGGL((pass_c_mr<R7>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
 }
 
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
@@ -1023,9 +1122,10 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        const MrArgs m = mr_args(p, a);
-        hipLaunchKernelGGL(pass_a_mr<1>, dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
-        hipLaunchKernelGGL(pass_b_mr<1>, dim3(mr_rows(p, 1), 2), dim3(64), mr_lds_b(p, 1), s, m);
+        if (p->r7)
+            mr_ir<true>(p, a, s);
+        else
+            mr_ir<false>(p, a, s);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
@@ -1034,7 +1134,13 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
 }
 
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
-                    hipStream_t s) {
+                    const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
+    const bool with_ir = d_ir_left && d_ir_right;
+    if (with_ir && (!p->direct || n_frames < p->sr)) {  // spectra first, then the audio
+        const hipError_t e = conv_set_ir(p, d_ir_left, d_ir_right, s);
+        if (e != hipSuccess) return e;
+        return conv_run(p, d_in, n_frames, d_out_left, d_out_right, nullptr, nullptr, s);
+    }
     if (n_frames <= 0) return hipSuccess;
     const int64_t S = n_frames / p->sr;  // kernels.cu:413
     if (S == 0) {  // nothing convolved: the reference output stays zero
@@ -1067,12 +1173,15 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.out_l = d_out_left;
     a.out_r = d_out_right;
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
+    a.ir_l = d_ir_left;
+    a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        const MrArgs m = mr_args(p, a);
-        hipLaunchKernelGGL(pass_a_mr<0>, dim3(mr_tiles(p, 8), (unsigned)pairs), dim3(512), mr_lds_a(p, 8), s, m);
-        hipLaunchKernelGGL(pass_b_mr<0>, dim3(mr_rows(p, 4), (unsigned)pairs), dim3(256), mr_lds_b(p, 4), s, m);
-        hipLaunchKernelGGL(pass_c_mr, dim3(mr_tiles(p, 8), (unsigned)(2 * pairs)), dim3(512), mr_lds_c(p, 8), s, m);
+        if (p->r7)
+            mr_file<true>(p, a, pairs, with_ir, s);
+        else
+            mr_file<false>(p, a, pairs, with_ir, s);
+        return hipGetLastError();
     } else {
         hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
         launch_pass_b<0>(p, (unsigned)pairs, a, s);
@@ -1110,10 +1219,10 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        const MrArgs m = mr_args(p, a);
-        hipLaunchKernelGGL(pass_a_mr<2>, dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
-        hipLaunchKernelGGL(pass_b_mr<0>, dim3(mr_rows(p, 1), 1), dim3(64), mr_lds_b(p, 1), s, m);
-        hipLaunchKernelGGL(pass_c_mr, dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
+        if (p->r7)
+            mr_live<true>(p, a, s);
+        else
+            mr_live<false>(p, a, s);
     } else {
         hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
         launch_pass_b<0>(p, 1, a, s);

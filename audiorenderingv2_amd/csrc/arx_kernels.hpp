@@ -50,11 +50,13 @@ hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
 struct ConvPlan;  // opaque, defined in arx_conv.hip
 ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char* err, size_t errlen);
 void conv_plan_destroy(ConvPlan* p);
-// Spectra of the two IRs (device f32, ir_len each); must precede conv_run.
+// Spectra of the two IRs (device f32, ir_len each), kept for the following conv_run calls.
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s);
-// Device-resident file-mode convolution (kernels.cu:382-438 + AudioRenderer.cpp:706-711).
+// Device-resident file-mode convolution (kernels.cu:382-438 + AudioRenderer.cpp:706-711).  With
+// d_ir_left / d_ir_right the IR spectra are recomputed from them first (on the direct path inside
+// the audio's own column pass); with NULLs the spectra of the last conv_set_ir are used.
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
-                    hipStream_t s);
+                    const float* d_ir_left, const float* d_ir_right, hipStream_t s);
 const char* conv_plan_describe(const ConvPlan* p);
 // Live (mic) block: plans created with sample_rate = block length.  One block of n_in <= block
 // f64 samples, circular length-ir_len convolution with both IR spectra, / (ir_len/2), zipped
