@@ -348,6 +348,8 @@ def main(argv=None) -> int:
     achieved = q_rank * bpb / (trace_ms * 1e-3) / 1e9
     traffic = load_profile("trace_traffic.json")
     counts = load_profile(os.path.join("r02", "trace_counts_c3.json"))
+    td = load_profile(os.path.join("r02", "trace_td_c3.json"))
+    conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02f.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
         "metric": METRIC,
@@ -400,8 +402,19 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": frames * BYTES_PER_STEREO_FRAME / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
+            "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and args.workload == "c3" else None,
+            "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and args.workload == "c3" else None,
+            "traffic_source": "profiles/r02/conv_traffic_r02f.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
+                              "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
+    if td and args.workload == "c3":
+        # the trace kernel's real ceiling: the texture-data (TD) return path, busy 0.9 of every CU-cycle
+        result["roofline_td"] = {
+            "kernel": "trace_kernel", "bound": "td", "achieved": td["td_busy_per_cu_cycle"], "peak": 1.0,
+            "unit": "TD busy cycles per CU-cycle", "frac": td["td_busy_per_cu_cycle"],
+            "ta_busy": td["ta_busy_per_cu_cycle"], "source": td["source"],
+        }
     if counts and args.workload == "c3":
         lanes = counts["lane_loads_16B_per_query"] * q_rank
         result["vector_memory"] = {
