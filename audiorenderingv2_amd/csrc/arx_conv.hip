@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "arx_kernels.hpp"
@@ -596,9 +597,9 @@ __device__ __forceinline__ void dft_radix(double2* x, int sign) {
 
 // One Stockham stage of radix R over buf[0..L) (LDS, this wave's row / column), Ns = product of
 // the earlier radices; twl = W_L^e.  Every lane first reads all its butterflies, then writes.
-template <int R>
+template <int R, int LM>
 __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L, int Ns, int j, int sign) {
-    constexpr int kMaxB = (kMaxSubLen / R + 63) / 64;
+    constexpr int kMaxB = (LM / R + 63) / 64;  // butterflies per lane for L <= LM
     const int nb = L / R, step = L / (Ns * R);
     double2 v[kMaxB][R];
 #pragma unroll
@@ -634,22 +635,103 @@ __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L
 
 // In-place FFT of buf[0..f.L) by one wave (lane j), natural order in and out.  R7: the plan has
 // radix-7 stages (their 7-point DFT costs ~20 VGPRs in every kernel that may run one).
-template <bool R7>
+template <bool R7, int LM>
 __device__ __forceinline__ void fft_mr_wave(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
     int Ns = 1;
     for (int s = 0; s < f.count; ++s) {
         switch (f.r[s]) {
-            case 8: mr_stage<8>(buf, twl, f.L, Ns, j, sign); break;
-            case 4: mr_stage<4>(buf, twl, f.L, Ns, j, sign); break;
-            case 2: mr_stage<2>(buf, twl, f.L, Ns, j, sign); break;
-            case 3: mr_stage<3>(buf, twl, f.L, Ns, j, sign); break;
-            case 5: mr_stage<5>(buf, twl, f.L, Ns, j, sign); break;
+            case 8: mr_stage<8, LM>(buf, twl, f.L, Ns, j, sign); break;
+            case 4: mr_stage<4, LM>(buf, twl, f.L, Ns, j, sign); break;
+            case 2: mr_stage<2, LM>(buf, twl, f.L, Ns, j, sign); break;
+            case 3: mr_stage<3, LM>(buf, twl, f.L, Ns, j, sign); break;
+            case 5: mr_stage<5, LM>(buf, twl, f.L, Ns, j, sign); break;
             default:
-                if constexpr (R7) mr_stage<7>(buf, twl, f.L, Ns, j, sign);
+                if constexpr (R7) mr_stage<7, LM>(buf, twl, f.L, Ns, j, sign);
                 break;
         }
         Ns *= f.r[s];
     }
+}
+
+// Compile-time plans for the sub-FFT lengths of the usual IRs (300 x 320 at 48 kHz, 160 x 200 at
+// 16 kHz, 315 x 280 at 44.1 kHz, 250 x 256 at 32 kHz): the same radix order as factor7, but every
+// stage's R, Ns and butterfly count are constants, so the index arithmetic (b mod Ns, twiddle
+// exponents, guards) folds away -- it was most of the generic stages' VALU work.
+constexpr int ct_radix(int L, int s) {
+    int v = L, t = 0;
+    while (v % 2 == 0) {
+        v /= 2;
+        ++t;
+    }
+    int idx = 0;
+    for (; t >= 3; t -= 3, ++idx)
+        if (idx == s) return 8;
+    if (t == 2 && idx++ == s) return 4;
+    if (t == 1 && idx++ == s) return 2;
+    for (int q = 3; q <= 7; q += 2)
+        while (v % q == 0) {
+            v /= q;
+            if (idx++ == s) return q;
+        }
+    return 0;  // past the last stage
+}
+constexpr int ct_ns(int L, int s) {
+    int ns = 1;
+    for (int i = 0; i < s; ++i) ns *= ct_radix(L, i);
+    return ns;
+}
+
+template <int R, int NS, int L>
+__device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, int j, int sign) {
+    constexpr int nb = L / R, step = L / (NS * R), kB = (nb + 63) / 64;
+    double2 v[kB][R];
+#pragma unroll
+    for (int i = 0; i < kB; ++i) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
+            const int k = b % NS;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                double2 x = buf[b + q * nb];
+                if (q > 0 && NS > 1) {
+                    const double2 w = twl[q * k * step];
+                    x = cmul(x, sign < 0 ? w : make_double2(w.x, -w.y));
+                }
+                v[i][q] = x;
+            }
+            dft_radix<R>(v[i], sign);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < kB; ++i) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
+            const int k = b % NS;
+            const int d = (b - k) * R + k;
+#pragma unroll
+            for (int q = 0; q < R; ++q) buf[d + q * NS] = v[i][q];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int L, int S>
+__device__ __forceinline__ void fft_ct_stages(double2* buf, const double2* twl, int j, int sign) {
+    if constexpr (ct_radix(L, S) != 0) {
+        mr_stage_ct<ct_radix(L, S), ct_ns(L, S), L>(buf, twl, j, sign);
+        fft_ct_stages<L, S + 1>(buf, twl, j, sign);
+    }
+}
+
+// In-place FFT of one row / column by one wave: the compile-time plan when L > 0, else the
+// run-time plan f (R7 / LM: see fft_mr_wave).
+template <bool R7, int LM, int L>
+__device__ __forceinline__ void fft_wave_any(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
+    if constexpr (L > 0)
+        fft_ct_stages<L, 0>(buf, twl, j, sign);
+    else
+        fft_mr_wave<R7, LM>(buf, twl, f, j, sign);
 }
 
 // Workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous run of tiles, so
@@ -665,36 +747,33 @@ struct MrArgs {
     int32_t fuse2;    // pass C: n == 2 sr and N1 even -- write the pair's odd output segment directly
 };
 
-constexpr int kMrIt = kMaxSubLen / 64;  // per-lane elements of one row / column, and per-thread tile loads
 
-// dst[i] = src[i * stride], i < count, by the nt threads (all loads issued before the LDS stores)
+// dst[i] = src[i * stride], i < count <= 64 IT, by the nt >= 64 threads (all loads issued before
+// the LDS stores)
+template <int IT>
 __device__ __forceinline__ void stage_table(double2* dst, const double2* __restrict__ src, int count, int stride,
                                             int nt) {
-    double2 v[kMrIt];
+    double2 v[IT];
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         v[it] = i < count ? src[(size_t)i * stride] : make_double2(0.0, 0.0);
     }
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         if (i < count) dst[i] = v[it];
     }
 }
 
-// W_n^e = W_N1^(e / N2) * W_n^(e mod N2) for e < n, from the LDS tables tq[q] = W_N1^q, tr[r] = W_n^r.
-__device__ __forceinline__ double2 tw_n(const double2* tq, const double2* tr, int e, int N2) {
-    const int q = e / N2;
-    return cmul(tq[q], tr[e - q * N2]);
-}
 
 // Pass A: forward column FFTs of length N1 (one wave per column, tc = waves per block), * W_n^(n2 k1),
 // stored transposed S[k1 N2 + n2].  LDS: tile tc x N1, W_N1 (N1), W_n^r (N2).  Mode 0 batches past
 // the block pairs (batch = n_pairs + c) are the IR channels c: their columns go to H, so the IR
 // spectra's column pass rides in the same launch as the audio's.
-template <int MODE, bool R7>
+template <int MODE, bool R7, int LM, int L1>
 __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
+    constexpr int IT = LM / 64;  // per-lane elements of a column, per-thread tile loads
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
     const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
@@ -704,9 +783,9 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
     double2* twl = lds + (size_t)tc * N1;
     double2* tr = twl + N1;
-    double2 v[kMrIt];
+    double2 v[IT];
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {  // every load in flight before the first use
+    for (int it = 0; it < IT; ++it) {  // every load in flight before the first use
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
         const int64_t idx = (int64_t)N2 * n1 + n2;
@@ -726,24 +805,34 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
         }
         v[it] = x;
     }
-    stage_table(twl, a.tw, N1, N2, nt);  // W_N1^i = W_n^(i N2)
-    stage_table(tr, a.tw, N2, 1, nt);
+    stage_table<IT>(twl, a.tw, N1, N2, nt);  // W_N1^i = W_n^(i N2)
+    stage_table<IT>(tr, a.tw, N2, 1, nt);
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), n1 = i >> lgc;
         if (n1 < N1) lds[(size_t)c * N1 + n1] = v[it];
     }
     __syncthreads();
-    fft_mr_wave<R7>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
+    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
     double2* dst = ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
+    // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r; this thread's column n2 is fixed and k1 steps
+    // by 64, so (q, r) advance by (64 n2) div / mod N2 -- one division per thread, not per element
+    const int c = threadIdx.x & (tc - 1), n2 = n2_0 + c;
+    const int k10 = threadIdx.x >> lgc;
+    const int step = 64 * n2, dq = step / N2, dr = step - dq * N2;
+    int q = (n2 * k10) / N2, r = n2 * k10 - q * N2;
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
-        const int i = threadIdx.x + it * nt;
-        const int c = i & (tc - 1), k1 = i >> lgc, n2 = n2_0 + c;
-        if (k1 < N1 && n2 < N2)
-            dst[(int64_t)k1 * N2 + n2] = cmul(lds[(size_t)c * N1 + k1], tw_n(twl, tr, n2 * k1, N2));
+    for (int it = 0; it < IT; ++it) {
+        const int k1 = k10 + 64 * it;
+        if (k1 < N1 && n2 < N2) dst[(int64_t)k1 * N2 + n2] = cmul(lds[(size_t)c * N1 + k1], cmul(twl[q], tr[r]));
+        q += dq;
+        r += dr;
+        if (r >= N2) {
+            r -= N2;
+            ++q;
+        }
     }
 }
 
@@ -751,8 +840,9 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
 // spectrum); mode 0 multiplies by H_c, inverse row FFT, * W_n^(-n2 k1), for both channels.
 // LDS: 2 x N2 per row (the spectrum; H_0's row, then the product), W_N2 (N2) -- small enough for
 // 3 blocks per CU, so one round of blocks covers the C3 grid.
-template <int MODE, bool R7>
+template <int MODE, bool R7, int LM, int L2>
 __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
+    constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
     const int nt = blockDim.x, rows = nt >> 6, N1 = a.N1, N2 = a.N2;
@@ -769,17 +859,22 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     double2* tw2 = lds + (size_t)rows * 2 * N2;
     const bool live = k1 < N1;
     double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
-    double2 v[kMrIt], h[kMrIt];
+    // every global operand of the row up front: the row, H_0 and H_1's rows and the four-step
+    // twiddles, so the wave's only global round trip before its stores is this one
+    double2 v[IT], h[IT], h1[IT], tw[IT];
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = j + 64 * it;
         const bool in = live && i < N2;
+        const bool in0 = MODE == 0 && in;
         v[it] = in ? row[i] : make_double2(0.0, 0.0);
-        h[it] = (MODE == 0 && in) ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);  // H_0's row
+        h[it] = in0 ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
+        h1[it] = in0 ? a.H[(size_t)a.M + (int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
+        tw[it] = in0 ? a.tw[(int64_t)i * k1] : make_double2(1.0, 0.0);  // W_n^(n2 k1), n2 k1 < n
     }
-    stage_table(tw2, a.tw, N2, N1, nt);  // W_N2^i = W_n^(i N1)
+    stage_table<IT>(tw2, a.tw, N2, N1, nt);  // W_N2^i = W_n^(i N1)
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = j + 64 * it;
         if (live && i < N2) {
             spec[i] = v[it];
@@ -788,32 +883,28 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     }
     __syncthreads();
     if (!live) return;  // no block barrier below
-    fft_mr_wave<R7>(spec, tw2, m.f2, j, -1);
+    fft_wave_any<R7, LM, L2>(spec, tw2, m.f2, j, -1);
     if (MODE == 1) {
 #pragma unroll
-        for (int it = 0; it < kMrIt; ++it) {
+        for (int it = 0; it < IT; ++it) {
             const int i = j + 64 * it;
             if (i < N2) row[i] = spec[i];
         }
         return;
     }
     for (int c = 0; c < 2; ++c) {
-        const double2* Hc = a.H + (size_t)c * a.M + (int64_t)k1 * N2;
 #pragma unroll
-        for (int it = 0; it < kMrIt; ++it) {
+        for (int it = 0; it < IT; ++it) {
             const int i = j + 64 * it;
-            if (i < N2) work[i] = cmul(spec[i], c == 0 ? work[i] : Hc[i]);
+            if (i < N2) work[i] = cmul(spec[i], c == 0 ? work[i] : h1[it]);
         }
         __builtin_amdgcn_wave_barrier();
-        fft_mr_wave<R7>(work, tw2, m.f2, j, +1);
+        fft_wave_any<R7, LM, L2>(work, tw2, m.f2, j, +1);
         double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
 #pragma unroll
-        for (int it = 0; it < kMrIt; ++it) {
+        for (int it = 0; it < IT; ++it) {
             const int i = j + 64 * it;
-            if (i < N2) {
-                const double2 t = a.tw[(int64_t)i * k1];  // W_n^(n2 k1), n2 k1 < n
-                dst[i] = cmul(work[i], make_double2(t.x, -t.y));
-            }
+            if (i < N2) dst[i] = cmul(work[i], make_double2(tw[it].x, -tw[it].y));
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -821,8 +912,9 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
 
 // Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
 // blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x N1, W_N1 (N1).
-template <bool R7>
+template <bool R7, int LM, int L1>
 __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
+    constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
     const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
@@ -831,22 +923,22 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
     const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
     double2* twl = lds + (size_t)tc * N1;
-    double2 v[kMrIt];
+    double2 v[IT];
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), k1 = i >> lgc, n2 = n2_0 + c;
         v[it] = (k1 < N1 && n2 < N2) ? src[(int64_t)k1 * N2 + n2] : make_double2(0.0, 0.0);
     }
-    stage_table(twl, a.tw, N1, N2, nt);
+    stage_table<IT>(twl, a.tw, N1, N2, nt);
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), k1 = i >> lgc;
         if (k1 < N1) lds[(size_t)c * N1 + k1] = v[it];
     }
     __syncthreads();
-    fft_mr_wave<R7>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
+    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
     __syncthreads();
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
     if (m.fuse2) {
@@ -860,7 +952,7 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
         double* E = a.Y + (pair * 2 + ch) * 2 * sr;
         double* F = E + sr;
 #pragma unroll
-        for (int it = 0; it < kMrIt; ++it) {
+        for (int it = 0; it < IT; ++it) {
             const int i = threadIdx.x + it * nt;
             const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
             if (n1 < half && n2 < N2) {
@@ -883,7 +975,7 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
     double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
 #pragma unroll
-    for (int it = 0; it < kMrIt; ++it) {
+    for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
         if (n1 < N1 && n2 < N2) {
@@ -1074,32 +1166,33 @@ static size_t mr_lds_a(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 +
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
-template <int MODE, bool R7>
+template <int MODE, bool R7, int LM, int L2>
 static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipStream_t s) {
     const unsigned groups8 = (mr_rows(p, rows) + 7) / 8 * 8;  // see pass_b_mr's XCD mapping
     m.batches = batches;
-    hipLaunchKernelGGL((pass_b_mr<MODE, R7>), dim3(groups8 * (unsigned)batches), dim3(64 * rows), mr_lds_b(p, rows), s,
+    hipLaunchKernelGGL((pass_b_mr<MODE, R7, LM, L2>), dim3(groups8 * (unsigned)batches), dim3(64 * rows), mr_lds_b(p, rows), s,
                        m);
 }
 
 // IR spectra alone (arx_prepare_ir_spectra, the live path)
-template <bool R7>
+template <bool R7, int LM, int L1, int L2>
 static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     const MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<1, R7>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
-    launch_b_mr<1, R7>(p, 1, 2, m, s);
+    hipLaunchKernelGGL((pass_a_mr<1, R7, LM, L1>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
+    launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
 }
 
 // File convolution; with_ir: the IR columns ride in pass A's launch as two extra batches.
-template <bool R7>
+template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<0, R7>), dim3(mr_tiles(p, 8), (unsigned)(pairs + (with_ir ? 2 : 0))), dim3(512),
-                       mr_lds_a(p, 8), s, m);
-    if (with_ir) launch_b_mr<1, R7>(p, 1, 2, m, s);
-    launch_b_mr<0, R7>(p, 4, (int)pairs, m, s);
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, 8), (unsigned)(pairs + (with_ir ? 2 : 0))),
+                       dim3(512), mr_lds_a(p, 8), s, m);
+    if (with_ir) launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
+    launch_b_mr<0, R7, LM, L2>(p, 4, (int)pairs, m, s);
     m.fuse2 = p->n == 2 * p->sr && p->N1 % 2 == 0;
-    hipLaunchKernelGGL((pass_c_mr<R7>), dim3(mr_tiles(p, 8), (unsigned)(2 * pairs)), dim3(512), mr_lds_c(p, 8), s, m);
+    hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, 4), (unsigned)(2 * pairs)), dim3(256), mr_lds_c(p, 4), s,
+                       m);
     const dim3 grid_d((unsigned)((a.len + kThreads - 1) / kThreads), 2);
     if (m.fuse2)
         hipLaunchKernelGGL(pass_d2, grid_d, dim3(kThreads), 0, s, a);
@@ -1107,12 +1200,39 @@ static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool wi
         hipLaunchKernelGGL(pass_d, grid_d, dim3(kThreads), 0, s, a);
 }
 
-template <bool R7>
+template <bool R7, int LM, int L1, int L2>
 static void mr_live(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     const MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<2, R7>), dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
-    launch_b_mr<0, R7>(p, 1, 1, m, s);
-    hipLaunchKernelGGL((pass_c_mr<R7>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
+    hipLaunchKernelGGL((pass_a_mr<2, R7, LM, L1>), dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
+    launch_b_mr<0, R7, LM, L2>(p, 1, 1, m, s);
+    hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
+}
+
+// The kernels exist for the sub-FFT pairs with compile-time plans (fft_ct_stages) and, for any
+// other split, for sub-FFT lengths <= 320 / <= 512 with and without radix-7 stages.
+template <typename Fn>
+static void mr_dispatch(const ConvPlan* p, Fn&& fn) {
+    using std::integral_constant;
+    const int N1 = p->N1, N2 = p->N2;
+    if (N1 == 300 && N2 == 320)
+        fn(std::false_type{}, integral_constant<int, 320>{}, integral_constant<int, 300>{}, integral_constant<int, 320>{});
+    else if (N1 == 160 && N2 == 200)
+        fn(std::false_type{}, integral_constant<int, 320>{}, integral_constant<int, 160>{}, integral_constant<int, 200>{});
+    else if (N1 == 315 && N2 == 280)
+        fn(std::true_type{}, integral_constant<int, 320>{}, integral_constant<int, 315>{}, integral_constant<int, 280>{});
+    else if (N1 == 250 && N2 == 256)
+        fn(std::false_type{}, integral_constant<int, 320>{}, integral_constant<int, 250>{}, integral_constant<int, 256>{});
+    else if (std::max(N1, N2) <= 320) {
+        if (p->r7)
+            fn(std::true_type{}, integral_constant<int, 320>{}, integral_constant<int, 0>{}, integral_constant<int, 0>{});
+        else
+            fn(std::false_type{}, integral_constant<int, 320>{}, integral_constant<int, 0>{}, integral_constant<int, 0>{});
+    } else {
+        if (p->r7)
+            fn(std::true_type{}, integral_constant<int, 512>{}, integral_constant<int, 0>{}, integral_constant<int, 0>{});
+        else
+            fn(std::false_type{}, integral_constant<int, 512>{}, integral_constant<int, 0>{}, integral_constant<int, 0>{});
+    }
 }
 
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
@@ -1122,10 +1242,9 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        if (p->r7)
-            mr_ir<true>(p, a, s);
-        else
-            mr_ir<false>(p, a, s);
+        mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
+            mr_ir<decltype(r7)::value, decltype(lm)::value, decltype(l1)::value, decltype(l2)::value>(p, a, s);
+        });
         return hipGetLastError();
     }
     hipLaunchKernelGGL(pass_a<1>, dim3(p->N2 / p->tc, 2), dim3(kThreads), lds_a, s, a);
@@ -1177,10 +1296,10 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.ir_r = d_ir_right;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        if (p->r7)
-            mr_file<true>(p, a, pairs, with_ir, s);
-        else
-            mr_file<false>(p, a, pairs, with_ir, s);
+        mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
+            mr_file<decltype(r7)::value, decltype(lm)::value, decltype(l1)::value, decltype(l2)::value>(p, a, pairs,
+                                                                                                        with_ir, s);
+        });
         return hipGetLastError();
     } else {
         hipLaunchKernelGGL(pass_a<0>, dim3(p->N2 / p->tc, (unsigned)pairs), dim3(kThreads), lds_a, s, a);
@@ -1219,10 +1338,9 @@ hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* 
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // Z2D (x n) / (ir_len/2)
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
-        if (p->r7)
-            mr_live<true>(p, a, s);
-        else
-            mr_live<false>(p, a, s);
+        mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
+            mr_live<decltype(r7)::value, decltype(lm)::value, decltype(l1)::value, decltype(l2)::value>(p, a, s);
+        });
     } else {
         hipLaunchKernelGGL(pass_a<2>, dim3(p->N2 / p->tc, 1), dim3(kThreads), lds_a, s, a);
         launch_pass_b<0>(p, 1, a, s);
