@@ -84,11 +84,32 @@ __device__ __forceinline__ double2 twiddle(const double2* __restrict__ tw, int32
     return sign < 0 ? w : make_double2(w.x, -w.y);
 }
 
+// Twiddle sources for lds_fft: W_M^e from one table of M entries, or (TwSplit) the product of two
+// small LDS tables hi[e >> lgLo] = W_M^(e & ~(2^lgLo - 1)) and lo[e & (2^lgLo - 1)] = W_M^(e mod 2^lgLo),
+// for transforms whose full table would not fit in LDS beside the data.
+struct TwFlat {
+    const double2* tw;
+    int32_t M;
+    __device__ double2 operator()(int64_t e, int sign) const { return twiddle(tw, M, e, sign); }
+};
+struct TwSplit {
+    const double2* hi;
+    const double2* lo;
+    int32_t lgLo, M;
+    __device__ double2 operator()(int64_t e, int sign) const {
+        const int64_t m = e & (M - 1);
+        const double2 w = cmul(hi[m >> lgLo], lo[m & ((1 << lgLo) - 1)]);
+        return sign < 0 ? w : make_double2(w.x, -w.y);
+    }
+};
+
 // In-place Stockham FFT of length L = 2^lg on buf[0..L) (LDS), executed by the nt
 // threads t in [0, nt) of this group; every thread of the workgroup must call it (it
 // contains __syncthreads()).  Twiddle W_L^e = tw[e * (M/L)].
 __device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, const double2* __restrict__ tw,
-                        int32_t M) {
+                        int32_t M);
+template <class TW>
+__device__ void lds_fft_t(double2* buf, int L, int lg, int sign, int t, int nt, const TW& twf, int32_t M) {
     const int mstep = M >> lg;  // M / L
     int Ns = 1;
     int stages4 = lg >> 1;
@@ -105,7 +126,7 @@ __device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, co
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     double2 x = buf[j + r * quarter];
-                    if (r > 0) x = cmul(x, twiddle(tw, M, (int64_t)r * k * (L / (Ns * 4)) * mstep, sign));
+                    if (r > 0) x = cmul(x, twf((int64_t)r * k * (L / (Ns * 4)) * mstep, sign));
                     v[b][r] = x;
                 }
             }
@@ -141,7 +162,7 @@ __device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, co
             if (j < half) {
                 const int k = j & (Ns - 1);
                 v[b][0] = buf[j];
-                v[b][1] = cmul(buf[j + half], twiddle(tw, M, (int64_t)k * (L / (Ns * 2)) * mstep, sign));
+                v[b][1] = cmul(buf[j + half], twf((int64_t)k * (L / (Ns * 2)) * mstep, sign));
             }
         }
         __syncthreads();
@@ -157,6 +178,11 @@ __device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, co
         }
         __syncthreads();
     }
+}
+
+__device__ void lds_fft(double2* buf, int L, int lg, int sign, int t, int nt, const double2* __restrict__ tw,
+                        int32_t M) {
+    lds_fft_t(buf, L, lg, sign, t, nt, TwFlat{tw, M}, M);
 }
 
 // ---- 512-point FFTs (the 48 kHz plans): one wave per row / column, radix-8 in registers ----
@@ -1379,6 +1405,19 @@ namespace {
 
 constexpr int kStreamThreads = 1024;  // lds_fft needs >= N/16 threads
 
+// The stream kernels' twiddles: W_N^e = hi[e >> 6] * lo[e & 63] from two small tables staged in LDS
+// after the N-point buffer (a global table lookup per butterfly put an L2 round trip into every
+// stage of these single-workgroup FFTs).
+__device__ __forceinline__ TwSplit stream_twiddles(double2* lds, int32_t N, int32_t lgN, const double2* __restrict__ tw) {
+    const int lgLo = lgN < 6 ? lgN : 6;
+    double2* hi = lds + N;
+    double2* lo = hi + (N >> lgLo);
+    for (int i = threadIdx.x; i < (N >> lgLo); i += kStreamThreads) hi[i] = tw[(size_t)i << lgLo];
+    for (int i = threadIdx.x; i < (1 << lgLo); i += kStreamThreads) lo[i] = tw[i];
+    return TwSplit{hi, lo, lgLo, N};
+}
+static size_t stream_lds(int32_t N) { return ((size_t)N + (size_t)(N >> 4) + 64) * sizeof(double2); }
+
 // G_p = FFT_N(hL[pB + i] + i hR[pB + i], i < B, zero padded): one workgroup per partition.
 __global__ __launch_bounds__(kStreamThreads) void stream_ir_kernel(const float* __restrict__ hl,
                                                                    const float* __restrict__ hr, int32_t n,
@@ -1391,8 +1430,9 @@ __global__ __launch_bounds__(kStreamThreads) void stream_ir_kernel(const float* 
         const int64_t k = (int64_t)p * B + i;
         buf[i] = (i < B && k < n) ? make_double2((double)hl[k], (double)hr[k]) : make_double2(0.0, 0.0);
     }
+    const TwSplit twf = stream_twiddles(buf, N, lgN, tw);
     __syncthreads();
-    lds_fft(buf, N, lgN, -1, threadIdx.x, kStreamThreads, tw, N);
+    lds_fft_t(buf, N, lgN, -1, threadIdx.x, kStreamThreads, twf, N);
     for (int i = threadIdx.x; i < N; i += kStreamThreads) G[(size_t)p * N + i] = buf[i];
 }
 
@@ -1409,9 +1449,10 @@ __global__ __launch_bounds__(kStreamThreads) void stream_fwd_kernel(const double
         else v = (i - H < n_in) ? in[i - H] : 0.0;
         buf[i] = make_double2(v, 0.0);
     }
+    const TwSplit twf = stream_twiddles(buf, N, lgN, tw);
     __syncthreads();
     for (int i = threadIdx.x; i < H; i += kStreamThreads) hist[i] = buf[i + B].x;
-    lds_fft(buf, N, lgN, -1, threadIdx.x, kStreamThreads, tw, N);  // (its first barrier orders the reads above)
+    lds_fft_t(buf, N, lgN, -1, threadIdx.x, kStreamThreads, twf, N);  // (its first barrier orders the reads above)
     for (int i = threadIdx.x; i < N; i += kStreamThreads) X[i] = buf[i];
 }
 
@@ -1440,8 +1481,9 @@ __global__ __launch_bounds__(kStreamThreads) void stream_inv_kernel(const double
                                                                     double* __restrict__ out) {
     extern __shared__ double2 buf[];
     for (int i = threadIdx.x; i < N; i += kStreamThreads) buf[i] = Z[i];
+    const TwSplit twf = stream_twiddles(buf, N, lgN, tw);
     __syncthreads();
-    lds_fft(buf, N, lgN, +1, threadIdx.x, kStreamThreads, tw, N);
+    lds_fft_t(buf, N, lgN, +1, threadIdx.x, kStreamThreads, twf, N);
     for (int i = threadIdx.x; i < B; i += kStreamThreads) {
         const double2 v = buf[N - B + i];
         out[2 * i] = v.x * scale;
@@ -1507,7 +1549,7 @@ hipError_t stream_reset(StreamPlan* p, hipStream_t s) {
 
 hipError_t stream_set_ir(StreamPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
     (void)hipGetLastError();  // report this launch's error, not a stale one
-    hipLaunchKernelGGL(stream_ir_kernel, dim3(p->P), dim3(kStreamThreads), (size_t)p->N * sizeof(double2), s, d_ir_left,
+    hipLaunchKernelGGL(stream_ir_kernel, dim3(p->P), dim3(kStreamThreads), stream_lds(p->N), s, d_ir_left,
                        d_ir_right, p->n, p->B, p->N, p->lgN, p->d_tw, p->d_G);
     return hipGetLastError();
 }
@@ -1516,7 +1558,7 @@ hipError_t stream_run(StreamPlan* p, const double* d_in, int64_t n_in, double* d
     (void)hipGetLastError();  // report this launch's error, not a stale one
     if (n_in < 0 || n_in > p->B) return hipErrorInvalidValue;
     const int32_t slot = (int32_t)(p->blocks % p->P);
-    const size_t lds = (size_t)p->N * sizeof(double2);
+    const size_t lds = stream_lds(p->N);
     hipLaunchKernelGGL(stream_fwd_kernel, dim3(1), dim3(kStreamThreads), lds, s, d_in, (int32_t)n_in, p->d_hist, p->B,
                        p->N, p->lgN, p->d_tw, p->d_X + (size_t)slot * p->N);
     hipLaunchKernelGGL(stream_mac_kernel, dim3((unsigned)((p->N + 255) / 256)), dim3(256), 0, s, p->d_X, p->d_G, p->P,
