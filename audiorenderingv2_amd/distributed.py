@@ -33,9 +33,11 @@ def env_rank_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str | None = None) -> tuple[int, int, int]:
+def init(backend: str | None = None, force: bool = False) -> tuple[int, int, int]:
+    """Join the process group when launched with WORLD_SIZE > 1 (or always with force=True: a
+    one-rank group, to rehearse the multi-process path on one GPU)."""
     rank, world, local = env_rank_world()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -50,25 +52,25 @@ def allreduce_histogram(hist: torch.Tensor) -> torch.Tensor:
     """In-place exact SUM of the int64 IR histograms of all ranks."""
     if hist.dtype != torch.int64:
         raise TypeError("IR histogram must be int64 fixed point")
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(hist, op=dist.ReduceOp.SUM)
     return hist
 
 
 def broadcast_object(objs: list, src: int = 0) -> list:
     """In-place broadcast of a list of picklable objects from rank src (e.g. the RCCL unique id)."""
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.broadcast_object_list(objs, src=src)
     return objs
 
 
 def barrier() -> None:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.barrier()
 
 
 def max_over_ranks(value: float, device: torch.device | None = None) -> float:
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -76,7 +78,7 @@ def max_over_ranks(value: float, device: torch.device | None = None) -> float:
 
 
 def sum_over_ranks(value: int, device: torch.device | None = None) -> int:
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not dist.is_initialized():
         return value
     t = torch.tensor([value], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)

@@ -257,6 +257,9 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
+    ap.add_argument("--process-group", action="store_true",
+                    help="join a torch.distributed group and take the one-GPU-per-process (RCCL rank) path even "
+                         "at one rank: a rehearsal of the N > 1 path on a one-GPU box")
     args = ap.parse_args(argv)
 
     import torch
@@ -265,7 +268,9 @@ def main(argv=None) -> int:
     from audiorenderingv2_amd import distributed as D
     from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, reference_audio
 
-    rank, world, local = D.init()
+    with _stdout_to_stderr():  # an eager RCCL init prints its version banner on stdout
+        rank, world, local = D.init(force=args.process_group)
+    import torch.distributed as dist
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (HIP); there is no CPU fallback")
     torch.cuda.set_device(local)
@@ -284,7 +289,7 @@ def main(argv=None) -> int:
     scene = conference_standin()
     receiver = receiver_local()
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
-        if world > 1:  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
+        if dist.is_initialized():  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
             uid = [RenderGroup.unique_id() if rank == 0 else None]
             D.broadcast_object(uid)
             g = RenderGroup.rank(settings, world, rank, uid[0], scene=scene, receiver=receiver)
@@ -438,9 +443,7 @@ def main(argv=None) -> int:
     if rank == 0:
         print(json.dumps(result), flush=True)
     g.close()
-    if world > 1:
-        import torch.distributed as dist
-
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 
