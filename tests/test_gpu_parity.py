@@ -336,7 +336,8 @@ def sparse_ir(n, rng, k=300, scale=1e-4):
 @pytest.mark.parametrize("sr,secs,length", [(1000, 2, 10555), (1000, 2, 999), (1000, 2, 4000), (800, 3, 7777),
                                             (16000, 2, 128000), (441, 2, 5000), (32000, 2, 70000),
                                             (22050, 1, 50000), (44100, 2, 100000), (1125, 2, 9000),
-                                            (1100, 2, 6000), (48000, 1, 100000)])
+                                            (1100, 2, 6000), (48000, 1, 100000), (96000, 2, 250000),
+                                            (77175, 2, 200000)])
 def test_convolution_matches_oracle(sr, secs, length):
     rng = np.random.default_rng(sr + length)
     n = sr * secs
