@@ -146,6 +146,10 @@ arx_status prepare_receiver_model(arx_renderer* r) {
     }
     start.push_back((int32_t)order.size());
     r->recv_levels = r->recv.nodes.empty() ? 0 : (int32_t)start.size() - 1;
+    if (receiver_refit_lds((int32_t)r->recv.tris.size(), (int32_t)r->recv.nodes.size(), r->recv_levels) > 160 * 1024) {
+        r->recv_refit = false;  // beyond one workgroup's LDS: rebuilt on the host per move instead
+        return ARX_OK;
+    }
     hipFree(r->d_recv_local);
     hipFree(r->d_recv_nodes);
     hipFree(r->d_recv_levels);

@@ -28,8 +28,9 @@ arx_status fail(arx_status s, const char* fmt, ...) __attribute__((format(printf
 // device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4..5] counting builds
 // [6] receiver refit left the quantization grid
 constexpr int kCounters = 8;
-// receivers up to this many triangles are moved by the device refit (its LDS holds 9 floats per
-// triangle and 6 per node); larger ones are rebuilt on the host per move
+// receivers up to this many triangles (and whose refit fits one workgroup's LDS: 9 floats per
+// triangle, 11 words per node) are moved by the device refit; larger ones are rebuilt on the host
+// per move
 constexpr int64_t kRefitMaxTris = 3000;
 
 inline uint64_t n_rays(const arx_config& c) {

@@ -43,7 +43,7 @@ struct RefitArgs {
     QNode2* qnodes;             // null: the quantized copy is not maintained (receiver off the grid)
     unsigned int* flag;         // set if a box fell off the grid (never, given the host's bound)
 };
-size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes);
+size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels);  // bytes of LDS
 hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
 
 // ---- convolution (arx_conv.hip) ----

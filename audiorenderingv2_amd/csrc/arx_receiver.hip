@@ -28,17 +28,20 @@ __device__ __forceinline__ int32_t child_code(int32_t ref, int32_t count) {
 }
 
 // Outward 16-bit grid index of a plane with the 0.1-step margin (quantize_nodes16, arx_bvh.cpp).
-__device__ __forceinline__ bool quantize_axis(const QGrid& g, int k, float lo, float hi, uint32_t& word) {
-    const double l = floor(((double)lo - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
-    const double h = ceil(((double)hi - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
+// inv = 1 / scale (f64): the product differs from the quotient by a few f64 ulps, far inside the
+// 0.1-step margin, so the planes stay conservative.
+__device__ __forceinline__ bool quantize_axis(const QGrid& g, const double* inv, int k, float lo, float hi,
+                                              uint32_t& word) {
+    const double l = floor(((double)lo - (double)g.origin[k]) * inv[k] - 0.1);
+    const double h = ceil(((double)hi - (double)g.origin[k]) * inv[k] + 0.1);
     if (!(l >= 0.0) || !(h <= 65535.0)) return false;
     word = (uint32_t)l | ((uint32_t)h << 16);
     return true;
 }
 
 // Box (lo, hi) of child c, unpadded, into the node's coded f32 form (padded) and its quantized half.
-__device__ void write_child(const RefitArgs& a, int32_t node, int c, const float* lo, const float* hi, int32_t code,
-                            bool empty) {
+__device__ void write_child(const RefitArgs& a, const double* inv, int32_t node, int c, const float* lo,
+                            const float* hi, int32_t code, bool empty) {
     BvhNode* n = a.cnodes + node;
     float* ab = c == 0 ? n->a : n->b;
     if (empty) {  // the inverted box of empty_child(): never passes the slab test
@@ -55,7 +58,7 @@ __device__ void write_child(const RefitArgs& a, int32_t node, int c, const float
     QChild& q = a.qnodes[node].c[c];
     for (int k = 0; k < 3; ++k) {
         uint32_t w = 1u;  // empty: the slab between planes 0 and 1 (quantize_nodes16)
-        if (!empty && !quantize_axis(a.grid, k, lo[k] - a.pad, hi[k] + a.pad, w)) {
+        if (!empty && !quantize_axis(a.grid, inv, k, lo[k] - a.pad, hi[k] + a.pad, w)) {
             atomicOr(a.flag, 1u);  // off the grid: the host's bound should have prevented it
             w = 0u | (65535u << 16);
         }
@@ -64,13 +67,62 @@ __device__ void write_child(const RefitArgs& a, int32_t node, int c, const float
     q.code = code;
 }
 
+constexpr int kRefitBatch = 4;  // global loads each thread keeps in flight
+
+__device__ __forceinline__ size_t refit_nd_offset(int32_t n_tris, int32_t n_nodes) {  // in floats, 16-B aligned
+    return ((size_t)9 * n_tris + (size_t)6 * n_nodes + 3) & ~(size_t)3;
+}
+
 __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs a) {
     extern __shared__ float lds[];
     float* wv = lds;                   // world vertices, 9 per receiver triangle
     float* nb = lds + 9 * a.n_tris;    // node boxes (lo xyz, hi xyz), unpadded
+    int4* nd = reinterpret_cast<int4*>(lds + refit_nd_offset(a.n_tris, a.n_nodes));  // child (ref, count) pairs
+    const double inv[3] = {1.0 / (double)a.grid.scale[0], 1.0 / (double)a.grid.scale[1], 1.0 / (double)a.grid.scale[2]};
+    int32_t* lnodes = reinterpret_cast<int32_t*>(nd + a.n_nodes);                     // the level schedule
+    int32_t* lstart = lnodes + a.n_nodes;
+    // 0. the nodes' child records and the level schedule into LDS, so the level loop below makes no
+    //    global round trips
+    for (int i = threadIdx.x; i <= a.n_levels; i += kRefitThreads) lstart[i] = a.level_start[i];
+    for (int i0 = threadIdx.x; i0 < a.n_nodes; i0 += kRefitBatch * kRefitThreads) {
+        int32_t l[kRefitBatch];
+#pragma unroll
+        for (int k = 0; k < kRefitBatch; ++k) {
+            const int i = i0 + k * kRefitThreads;
+            l[k] = i < a.n_nodes ? a.level_nodes[i] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kRefitBatch; ++k) {
+            const int i = i0 + k * kRefitThreads;
+            if (i < a.n_nodes) lnodes[i] = l[k];
+        }
+    }
+    for (int i0 = threadIdx.x; i0 < a.n_nodes; i0 += kRefitBatch * kRefitThreads) {
+        int4 v[kRefitBatch];
+#pragma unroll
+        for (int k = 0; k < kRefitBatch; ++k) {
+            const int i = i0 + k * kRefitThreads;
+            v[k] = i < a.n_nodes ? *reinterpret_cast<const int4*>(a.local_nodes[i].d) : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < kRefitBatch; ++k) {
+            const int i = i0 + k * kRefitThreads;
+            if (i < a.n_nodes) nd[i] = v[k];
+        }
+    }
     // 1. transform (OptixModel.cpp:178-193 with glm's operation order, as arx_place_receiver_vertices)
-    for (int i = threadIdx.x; i < a.n_tris; i += kRefitThreads) {
-        const TriRec src = a.local_tris[i];
+    for (int i0 = threadIdx.x; i0 < a.n_tris; i0 += kRefitBatch * kRefitThreads) {
+      TriRec pre[kRefitBatch];
+#pragma unroll
+      for (int k = 0; k < kRefitBatch; ++k) {
+          const int i = i0 + k * kRefitThreads;
+          if (i < a.n_tris) pre[k] = a.local_tris[i];
+      }
+#pragma unroll
+      for (int k = 0; k < kRefitBatch; ++k) {
+        const int i = i0 + k * kRefitThreads;
+        if (i >= a.n_tris) break;
+        const TriRec src = pre[k];
         TriRec dst = src;
         const float* v[3] = {src.v0, src.v1, src.v2};
         float* o[3] = {dst.v0, dst.v1, dst.v2};
@@ -87,6 +139,7 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
             wv[9 * i + 3 * j + 2] = o[j][2];
         }
         a.tris[a.tri_base + i] = dst;
+      }
     }
     __syncthreads();
     // box of a child reference (global refs): a leaf's triangles or an already refit node
@@ -112,16 +165,17 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
     };
     // 2. bottom-up refit, deepest level first (fixed topology)
     for (int L = 0; L < a.n_levels; ++L) {
-        for (int i = a.level_start[L] + threadIdx.x; i < a.level_start[L + 1]; i += kRefitThreads) {
-            const int32_t ln = a.level_nodes[i];
-            const BvhNode src = a.local_nodes[ln];
+        for (int i = lstart[L] + threadIdx.x; i < lstart[L + 1]; i += kRefitThreads) {
+            const int32_t ln = lnodes[i];
+            const int4 d4 = nd[ln];
+            const int32_t sd[4] = {d4.x, d4.y, d4.z, d4.w};
             float blo[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
             float bhi[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
             for (int c = 0; c < 2; ++c) {
-                const int32_t ref = src.d[c], count = src.d[2 + c];
+                const int32_t ref = sd[c], count = sd[2 + c];
                 float lo[3], hi[3];
                 child_box(ref, count, lo, hi);
-                write_child(a, a.node_base + ln, c, lo, hi, child_code(ref, count), count < 0);
+                write_child(a, inv, a.node_base + ln, c, lo, hi, child_code(ref, count), count < 0);
                 for (int k = 0; k < 3; ++k) {
                     blo[k] = fminf(blo[k], lo[k]);
                     bhi[k] = fmaxf(bhi[k], hi[k]);
@@ -138,17 +192,21 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
     if (threadIdx.x == 0) {
         float lo[3], hi[3];
         child_box(a.root_ref, a.root_count, lo, hi);
-        write_child(a, 0, 1, lo, hi, child_code(a.root_ref, a.root_count), a.root_count < 0);
+        write_child(a, inv, 0, 1, lo, hi, child_code(a.root_ref, a.root_count), a.root_count < 0);
     }
 }
 
 }  // namespace
 
-size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes) { return ((size_t)9 * n_tris + (size_t)6 * n_nodes) * 4; }
+size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels) {
+    return ((((size_t)9 * n_tris + (size_t)6 * n_nodes + 3) & ~(size_t)3) + (size_t)5 * n_nodes + (size_t)n_levels + 1) *
+           4;
+}
 
 hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(receiver_refit_kernel, dim3(1), dim3(kRefitThreads), receiver_refit_lds(a.n_tris, a.n_nodes), s,
+    hipLaunchKernelGGL(receiver_refit_kernel, dim3(1), dim3(kRefitThreads), receiver_refit_lds(a.n_tris, a.n_nodes, a.n_levels),
+                       s,
                        a);
     return hipGetLastError();
 }
