@@ -44,6 +44,15 @@ def write_obj(path, meshes, mtl_name):
         fh.write("".join(f"newmtl {n}\n" for n in sorted({m.name for m in meshes})))
 
 
+def write_receivers(d):
+    from audiorenderingv2_amd.scene import Mesh
+
+    L, R = receiver_local()
+    for tris, fn in ((L, "leftHalf.obj"), (R, "rightHalf.obj")):
+        v = tris.reshape(-1, 3)
+        write_obj(str(d / fn), [Mesh("half", v, np.arange(v.shape[0], dtype=np.int32).reshape(-1, 3))], fn + ".mtl")
+
+
 @pytest.fixture(scope="module")
 def demo(tmp_path_factory):
     gxx = shutil.which("g++")
@@ -62,12 +71,7 @@ def test_cpp_shim_export_flow_matches_oracle(demo):
     d, exe = demo
     meshes = load_meshes_npz(os.path.join(GOLDEN, "test_obj.npz"))  # R/test.obj as the reference's tinyobj read it
     write_obj(str(d / "room.obj"), meshes, "room.mtl")
-    from audiorenderingv2_amd.scene import Mesh
-
-    L, R = receiver_local()
-    for name, tris, fn in (("receiver_left", L, "leftHalf.obj"), ("receiver_right", R, "rightHalf.obj")):
-        v = tris.reshape(-1, 3)
-        write_obj(str(d / fn), [Mesh("half", v, np.arange(v.shape[0], dtype=np.int32).reshape(-1, 3))], fn + ".mtl")
+    write_receivers(d)
     sr = 16000
     rng = np.random.default_rng(5)
     t = np.arange(3 * sr + 1234) / sr
@@ -120,3 +124,70 @@ def test_cpp_shim_export_flow_matches_oracle(demo):
         assert np.abs(live - ref).max() <= 1e-12 * np.abs(ref).max()
         results.append((gl, gr))
     assert np.array_equal(results[0][0], results[1][0]) and np.array_equal(results[0][1], results[1][1])
+
+
+def test_cpp_shim_c4_sharded_equals_python_group(demo):
+    """configs[3] through the C++ shim: the conference stand-in as an OBJ file, 10 M rays x 32
+    bounces at 48 kHz, 8 ray shards on the one GPU (group API).  Its IR must be bit-identical to the
+    Python RenderGroup's single-device render of the same OBJ (the configs[3] path that
+    tests/test_gpu_group.py::test_c4_sharded_group checks against the oracle on ray samples)."""
+    from audiorenderingv2_amd import RenderGroup, RenderSettings
+    from audiorenderingv2_amd.formats import load_scene
+    from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, conference_standin
+
+    d, exe = demo
+    write_receivers(d)
+    sc = conference_standin()
+    lines = ["mtllib conf.mtl"]
+    base = 1
+    start = 0
+    names = sc.names
+    while start < sc.n_tris:  # one OBJ object per run of equal material names
+        end = start
+        while end < sc.n_tris and names[end] == names[start]:
+            end += 1
+        lines.append(f"o part{start}")
+        v = sc.tri_v[start:end].reshape(-1, 3)
+        lines.extend("v %.9g %.9g %.9g" % tuple(p) for p in v.tolist())
+        lines.append(f"usemtl {names[start]}")
+        lines.extend(f"f {base + 3 * k} {base + 3 * k + 1} {base + 3 * k + 2}" for k in range(end - start))
+        base += v.shape[0]
+        start = end
+    (d / "conf.obj").write_text("\n".join(lines) + "\n")
+    (d / "conf.mtl").write_text("".join(f"newmtl {n}\n" for n in sorted(set(names))))
+    sr = 48000
+    x = (0.3 * np.sin(2 * np.pi * 440 * np.arange(2 * sr + 777) / sr)).astype(np.float32)
+    save_wav(str(d / "conf.wav"), x, sr, 32)
+    cfg = {
+        "renderer_parameters": {"ir_length_in_seconds": 2},
+        "scene_parameters": {"mono": False, "scene_file_path": str(d / "conf.obj"), "audio_file_path": str(d / "conf.wav"),
+                             "initial_receiver_pos": dict(zip("xyz", CONFERENCE_LISTENER)),
+                             "initial_emitter_pos": dict(zip("xyz", CONFERENCE_EMITTER))},
+        "pathtracer_parameters": {"base_power": 3.62, "rays": {"x": 1000, "y": 100, "z": 100},
+                                  "ray_energy_threshold": 0.0, "ray_max_bounces": 32, "hrtf_absorption_rate": 1.0,
+                                  "materials": []},
+    }
+    (d / "conf.json").write_text(json.dumps(cfg))
+    out = d / "out_c4"
+    out.mkdir()
+    run = subprocess.run([exe, str(d / "conf.json"), str(d / "leftHalf.obj"), str(d / "rightHalf.obj"), str(out),
+                          ",".join(["0"] * 8)], capture_output=True, text=True, timeout=200)
+    assert run.returncode == 0, run.stderr
+    line = [ln for ln in run.stdout.splitlines() if ln.startswith("queries ")][-1]
+    st = dict(zip(line.split()[::2], line.split()[1::2]))
+    assert int(st["gpus"]) == 8
+    # the same OBJ through the Python loader (the same native tinyobj restatement) and a one-GPU group
+    scene = load_scene(str(d / "conf.obj"))
+    s = RenderSettings(rays=(1000, 100, 100), sample_rate=sr, base_power=3.62, max_bounces=32,
+                       hrtf_absorption_rate=1.0, ir_length_in_seconds=2)
+    g = RenderGroup(s, devices=[0], scene=scene, receiver=receiver_local())
+    g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+    g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+    g.render()
+    gl, gr = g.get_ir()
+    gst = g.stats()
+    g.close()
+    assert int(st["queries"]) == gst["queries"] and int(st["receiver_hits"]) == gst["receiver_hits"]
+    assert 20 * 10_000_000 < gst["queries"] <= 32 * 10_000_000 and gst["receiver_hits"] > 10000
+    assert np.array_equal(np.fromfile(out / "ir_left.f32", np.float32).view(np.uint32), gl.view(np.uint32))
+    assert np.array_equal(np.fromfile(out / "ir_right.f32", np.float32).view(np.uint32), gr.view(np.uint32))
