@@ -1209,16 +1209,27 @@ static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
 }
 
 // File convolution; with_ir: the IR columns ride in pass A's launch as two extra batches.
+// Launch shapes (columns per block in A / C, rows per block in B); the ARX_CONV_* macros exist only
+// for design-experiment builds (build.py --exp).
+#ifndef ARX_CONV_TCA
+#define ARX_CONV_TCA 8
+#endif
+#ifndef ARX_CONV_TCC
+#define ARX_CONV_TCC 4
+#endif
+#ifndef ARX_CONV_ROWSB
+#define ARX_CONV_ROWSB 4
+#endif
 template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, 8), (unsigned)(pairs + (with_ir ? 2 : 0))),
-                       dim3(512), mr_lds_a(p, 8), s, m);
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)(pairs + (with_ir ? 2 : 0))),
+                       dim3(64 * ARX_CONV_TCA), mr_lds_a(p, ARX_CONV_TCA), s, m);
     if (with_ir) launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
-    launch_b_mr<0, R7, LM, L2>(p, 4, (int)pairs, m, s);
+    launch_b_mr<0, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
     m.fuse2 = p->n == 2 * p->sr && p->N1 % 2 == 0;
-    hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, 4), (unsigned)(2 * pairs)), dim3(256), mr_lds_c(p, 4), s,
-                       m);
+    hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), (unsigned)(2 * pairs)),
+                       dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
     const dim3 grid_d((unsigned)((a.len + kThreads - 1) / kThreads), 2);
     if (m.fuse2)
         hipLaunchKernelGGL(pass_d2, grid_d, dim3(kThreads), 0, s, a);
