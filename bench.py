@@ -354,6 +354,7 @@ def main(argv=None) -> int:
     traffic = load_profile("trace_traffic.json")
     counts = load_profile(os.path.join("r02", "trace_counts_c3.json"))
     td = load_profile(os.path.join("r02", "trace_td_c3.json"))
+    vmem = load_profile(os.path.join("r02", "trace_vmem_ceiling.json"))
     conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02g.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
@@ -413,6 +414,17 @@ def main(argv=None) -> int:
                               "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
+    if vmem and counts and args.workload == "c3":
+        # the trace's divergent 16-B gathers against their microbenchmark-calibrated ceiling for this
+        # kernel's L1 / L2 / Infinity-Cache hit mix (tools/vmem_ceiling.py)
+        lane_rate = counts["lane_loads_16B_per_query"] * q_rank / (trace_ms * 1e-3)
+        result["roofline_vmem"] = {
+            "kernel": "trace_kernel", "bound": "vector-memory gathers (L1/L2/Infinity-Cache mix)",
+            "achieved": lane_rate, "peak": vmem["ceiling_lane_loads_per_s"], "unit": "16-B lane loads/s",
+            "frac": lane_rate / vmem["ceiling_lane_loads_per_s"],
+            "mix": {"l1": vmem["fraction_l1"], "l2_hit": vmem["fraction_l2_hit"], "l2_miss": vmem["fraction_l2_miss"]},
+            "source": "profiles/r02/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix)",
+        }
     if td and args.workload == "c3":
         # the trace kernel's real ceiling: the texture-data (TD) return path, busy 0.9 of every CU-cycle
         result["roofline_td"] = {

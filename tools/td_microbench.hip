@@ -3,9 +3,9 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/td_microbench.hip -o /tmp/td_microbench && /tmp/td_microbench
 //
-// Every lane issues ITERS independent global_load_dwordx4 from a 16 MB table (L2 / Infinity-
-// Cache resident, like the BVH), with addresses drawn so that one wave-instruction touches
-// a chosen number of distinct 64-B blocks, with a chosen fraction of active lanes.
+// Every lane issues ITERS independent global_load_dwordx4 from a table of 16 KB ... 64 MB (L1,
+// L2, Infinity Cache resident), with addresses drawn so that one wave-instruction touches a
+// chosen number of distinct 64-B blocks, with a chosen fraction of active lanes.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -66,13 +66,6 @@ int main() {
         hipDeviceGetAttribute(&v[3], hipDeviceAttributeClockRate, 0);
         std::printf("lds per block %d, per CU %d, opt-in per block %d, clock %d kHz\n", v[0], v[1], v[2], v[3]);
     }
-    const size_t bytes = 16u << 20;
-    const uint32_t n_blocks = (uint32_t)(bytes / 64);
-    float4* table;
-    float* out;
-    hipMalloc(&table, bytes);
-    hipMalloc(&out, 4);
-    hipMemset(table, 0, bytes);
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int waves_per_cu = 20, block = 128;
@@ -80,6 +73,8 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    float* out;
+    hipMalloc(&out, 4);
     struct Case {
         const char* name;
         int mode, active;
@@ -90,22 +85,34 @@ int main() {
                  {"distinct blocks, 32 lanes active", 3, 32},
                  {"distinct blocks, 16 lanes active", 3, 16},
                  {"distinct blocks, 8 lanes active", 3, 8}};
-    for (const Case& c : cases) {
-        hipLaunchKernelGGL(gather, dim3(grid), dim3(block), 0, 0, table, n_blocks, c.mode, c.active, out);
-        hipEventRecord(e0);
-        const int reps = 5;
-        for (int r = 0; r < reps; ++r)
+    // table sizes: L1-resident, one XCD's L2 (4 MB) and below, Infinity Cache, beyond
+    const size_t sizes_kb[] = {16, 256, 2048, 16384, 65536};
+    for (size_t kb : sizes_kb) {
+        const size_t bytes = kb << 10;
+        const uint32_t n_blocks = (uint32_t)(bytes / 64);
+        float4* table;
+        hipMalloc(&table, bytes);
+        hipMemset(table, 0, bytes);
+        std::printf("-- table %zu KB\n", kb);
+        for (const Case& c : cases) {
+            if (kb != 16384 && c.mode != 0 && c.mode != 2) continue;  // the sharing sweep at 16 MB only
             hipLaunchKernelGGL(gather, dim3(grid), dim3(block), 0, 0, table, n_blocks, c.mode, c.active, out);
-        hipEventRecord(e1);
-        hipEventSynchronize(e1);
-        float ms = 0;
-        hipEventElapsedTime(&ms, e0, e1);
-        ms /= reps;
-        const double instr_per_cu = (double)waves_per_cu * ITERS;
-        const double cyc = ms * 1e-3 * 2.1e9;  // ~effective clock under load
-        const double lane_loads = (double)grid * block * ITERS * ((c.mode == 3) ? (double)c.active / 64.0 : 1.0);
-        std::printf("%-40s %.3f ms  %.1f cycles per wave-instruction per CU  %.4g 16-B lane loads/s\n", c.name, ms,
-                    cyc / instr_per_cu, lane_loads / (ms * 1e-3));
+            hipEventRecord(e0);
+            const int reps = 5;
+            for (int r = 0; r < reps; ++r)
+                hipLaunchKernelGGL(gather, dim3(grid), dim3(block), 0, 0, table, n_blocks, c.mode, c.active, out);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            ms /= reps;
+            const double instr_per_cu = (double)waves_per_cu * ITERS;
+            const double cyc = ms * 1e-3 * 2.1e9;  // ~effective clock under load
+            const double lane_loads = (double)grid * block * ITERS * ((c.mode == 3) ? (double)c.active / 64.0 : 1.0);
+            std::printf("%-40s %.3f ms  %.1f cycles per wave-instruction per CU  %.4g 16-B lane loads/s\n", c.name, ms,
+                        cyc / instr_per_cu, lane_loads / (ms * 1e-3));
+        }
+        hipFree(table);
     }
     return 0;
 }
