@@ -10,7 +10,7 @@ import os
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("ARX_LIB", os.path.join(_PKG, "libarx.so"))
+LIB_PATH = os.path.join(_PKG, "libarx.so")  # the product library (no environment override)
 
 ARX_OK = 0
 STATUS_NAMES = {
@@ -166,6 +166,16 @@ SIGNATURES = {
 
 _lib = None
 _lock = threading.Lock()
+
+
+def use_library(path: str) -> None:
+    """Design tools only (tools/*.py): bind a design-experiment build (build.py --exp) instead of
+    the product library; must precede the first call into the library."""
+    global LIB_PATH
+    with _lock:
+        if _lib is not None:
+            raise ArxError(6, "the library is already loaded")
+        LIB_PATH = path
 
 
 def lib() -> C.CDLL:

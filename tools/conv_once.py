@@ -12,6 +12,10 @@ import torch  # noqa: E402
 
 from audiorenderingv2_amd import AudioRenderer, RenderSettings  # noqa: E402
 from audiorenderingv2_amd.scene import reference_audio  # noqa: E402
+from audiorenderingv2_amd._lib import use_library  # noqa: E402
+
+if os.environ.get("ARX_LIB"):  # a design-experiment build (tools only)
+    use_library(os.environ["ARX_LIB"])
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 x, sr = reference_audio("clapper")

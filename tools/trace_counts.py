@@ -14,6 +14,10 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local  # noqa: E402
 from audiorenderingv2_amd._lib import check, lib  # noqa: E402
+from audiorenderingv2_amd._lib import use_library  # noqa: E402
+
+if os.environ.get("ARX_LIB"):  # a design-experiment build (tools only)
+    use_library(os.environ["ARX_LIB"])
 from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  # noqa: E402
 
 s = RenderSettings(rays=(100, 100, 100), sample_rate=48000, base_power=3.62, max_bounces=16)

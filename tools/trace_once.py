@@ -12,6 +12,10 @@ import numpy as np
 sys.path.insert(0, os.environ.get("ARX_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from audiorenderingv2_amd import AudioRenderer, RenderSettings, conference_standin, receiver_local  # noqa: E402
 from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER  # noqa: E402
+from audiorenderingv2_amd._lib import use_library  # noqa: E402
+
+if os.environ.get("ARX_LIB"):  # a design-experiment build (tools only)
+    use_library(os.environ["ARX_LIB"])
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 rays = tuple(int(v) for v in os.environ.get("RAYS", "100,100,100").split(","))
