@@ -107,6 +107,7 @@ SIGNATURES = {
     "arx_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),
     "arx_frac_bits": (C.c_int, [C.c_uint64]),
     "arx_set_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
+    "arx_set_ir_device": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_size_t]),
     "arx_convolute_audio_file": (C.c_int, [_P, _F, C.c_size_t, _F, _F, _D, _D]),
     "arx_convolute_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
     "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),

@@ -803,6 +803,18 @@ arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right
     return ARX_OK;
 }
 
+arx_status arx_set_ir_device(arx_renderer* r, const float* d_left, const float* d_right, size_t ir_len) {
+    if (!r || !d_left || !d_right) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (ir_len != (size_t)r->ir_len) return fail(ARX_ERR_INVALID_ARGUMENT, "ir_len %zu != %d", ir_len, r->ir_len);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipMemcpyAsync(r->d_ir, d_left, ir_len * sizeof(float), hipMemcpyDeviceToDevice, r->stream));
+    ARX_HIP(hipMemcpyAsync(r->d_ir + r->ir_len, d_right, ir_len * sizeof(float), hipMemcpyDeviceToDevice, r->stream));
+    r->conv_ir_dirty = true;
+    r->conv_live_ir_dirty = true;
+    ++r->ir_generation;
+    return ARX_OK;
+}
+
 // spectra = false: leave a changed IR's spectra to the next conv_run (which folds them into its
 // own first pass)
 static arx_status ensure_conv(arx_renderer* r, bool spectra = true) {

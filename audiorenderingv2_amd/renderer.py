@@ -248,6 +248,10 @@ class AudioRenderer:
         """Recompute the cached IR spectra now (async) rather than in the next convolution."""
         check(lib().arx_prepare_ir_spectra(self._h, (1 if file else 0) | (2 if live else 0)))
 
+    def set_ir_device(self, d_left: int, d_right: int) -> None:
+        """Take the IR from device memory (arx_set_ir_device), async on this renderer's stream."""
+        check(lib().arx_set_ir_device(self._h, C.c_void_p(d_left), C.c_void_p(d_right), self.ir_length))
+
     def conv_plan(self, live: bool = False) -> str:
         """The convolution plan in use (arx_conv_describe): direct mixed-radix or power-of-two."""
         buf = C.create_string_buffer(256)

@@ -142,6 +142,10 @@ arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out)
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */
 arx_status arx_set_ir(arx_renderer* r, const float* h_left, const float* h_right, size_t ir_len);
+/* Same from device memory on the renderer's device (e.g. another renderer's IR, arx_ir_device),
+ * asynchronous on the renderer's stream: the caller orders it after the IR's producer (a HIP
+ * event) and keeps the source unchanged until the copy has run. */
+arx_status arx_set_ir_device(arx_renderer* r, const float* d_left, const float* d_right, size_t ir_len);
 int arx_frac_bits(uint64_t n_rays_total);
 
 /* ---- Multi-GPU ray sharding ------------------------------------------------------------------

@@ -421,3 +421,23 @@ def test_rejects_absorption_and_hrtf_outside_unit_interval():
     r.set_scene(Scene(tv, np.array([0.0, 1.0], np.float32), []))
     with pytest.raises(ArxError):
         r.set_hrtf_absorption_rate(1.25)
+
+
+def test_set_ir_device_equals_set_ir():
+    """arx_set_ir_device: another renderer's IR taken by a device copy convolves like the same IR
+    set from the host."""
+    torch = pytest.importorskip("torch")
+    sr = 16000
+    rng = np.random.default_rng(11)
+    a, b = conv_renderer(sr), conv_renderer(sr)
+    irl, irr = sparse_ir(2 * sr, rng), sparse_ir(2 * sr, rng)
+    a.set_ir(irl, irr)
+    dl, dr, n = a.ir_device_ptrs()
+    assert n == 2 * sr
+    b.set_ir_device(dl, dr)
+    x = rng.standard_normal(3 * sr + 5).astype(np.float32)
+    La, Ra, _, _ = a.convoluteAudioFile(x)
+    Lb, Rb, _, _ = b.convoluteAudioFile(x)
+    assert np.array_equal(La, Lb) and np.array_equal(Ra, Rb)
+    gl, gr = b.get_ir()
+    assert np.array_equal(gl, irl) and np.array_equal(gr, irr)
