@@ -621,12 +621,23 @@ __device__ __forceinline__ void dft_radix(double2* x, int sign) {
     }
 }
 
+// LDS slot of element i of a sub-FFT buffer between its first two stages when SW: the elements'
+// 8-element blocks XOR-swizzled (block k's slots permuted by k mod 8; a tail short of a whole block
+// stays put).  The first stage of an even length stores with stride R in {2, 4, 8}: unswizzled, the 8
+// lanes of a ds_write_b128 group land on one or two 128-B bank rows (up to 8-way conflicts); swizzled
+// they cover all 8.  The second stage reads through the same map and stores in natural order.
+template <bool SW>
+__device__ __forceinline__ int lds_ix(int i, int L8) {
+    return (SW && i < L8) ? (i ^ ((i >> 3) & 7)) : i;
+}
+
 // One Stockham stage of radix R over buf[0..L) (LDS, this wave's row / column), Ns = product of
 // the earlier radices; twl = W_L^e.  Every lane first reads all its butterflies, then writes.
-template <int R, int LM>
+// SWI / SWO: the input / output is in the lds_ix swizzled order.
+template <int R, int LM, bool SWI, bool SWO>
 __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L, int Ns, int j, int sign) {
     constexpr int kMaxB = (LM / R + 63) / 64;  // butterflies per lane for L <= LM
-    const int nb = L / R, step = L / (Ns * R);
+    const int nb = L / R, step = L / (Ns * R), L8 = L & ~7;
     double2 v[kMaxB][R];
 #pragma unroll
     for (int i = 0; i < kMaxB; ++i) {
@@ -635,7 +646,7 @@ __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L
             const int k = b % Ns;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                double2 x = buf[b + q * nb];
+                double2 x = buf[lds_ix<SWI>(b + q * nb, L8)];
                 if (q > 0) {
                     const double2 w = twl[q * k * step];
                     x = cmul(x, sign < 0 ? w : make_double2(w.x, -w.y));
@@ -653,28 +664,40 @@ __device__ __forceinline__ void mr_stage(double2* buf, const double2* twl, int L
             const int k = b % Ns;
             const int d = (b - k) * R + k;
 #pragma unroll
-            for (int q = 0; q < R; ++q) buf[d + q * Ns] = v[i][q];
+            for (int q = 0; q < R; ++q) buf[lds_ix<SWO>(d + q * Ns, L8)] = v[i][q];
         }
     }
     __builtin_amdgcn_wave_barrier();
 }
 
+template <bool R7, int LM, bool SWI, bool SWO>
+__device__ __forceinline__ void mr_stage_r(int r, double2* buf, const double2* twl, int L, int Ns, int j, int sign) {
+    switch (r) {
+        case 8: mr_stage<8, LM, SWI, SWO>(buf, twl, L, Ns, j, sign); break;
+        case 4: mr_stage<4, LM, SWI, SWO>(buf, twl, L, Ns, j, sign); break;
+        case 2: mr_stage<2, LM, SWI, SWO>(buf, twl, L, Ns, j, sign); break;
+        case 3: mr_stage<3, LM, SWI, SWO>(buf, twl, L, Ns, j, sign); break;
+        case 5: mr_stage<5, LM, SWI, SWO>(buf, twl, L, Ns, j, sign); break;
+        default:
+            if constexpr (R7) mr_stage<7, LM, SWI, SWO>(buf, twl, L, Ns, j, sign);
+            break;
+    }
+}
+
 // In-place FFT of buf[0..f.L) by one wave (lane j), natural order in and out.  R7: the plan has
-// radix-7 stages (their 7-point DFT costs ~20 VGPRs in every kernel that may run one).
+// radix-7 stages (their 7-point DFT costs ~20 VGPRs in every kernel that may run one).  An even
+// length starts with its radix-2^k stages (factor7), so its first stage stores swizzled (lds_ix).
 template <bool R7, int LM>
 __device__ __forceinline__ void fft_mr_wave(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
+    const bool even = (f.L & 1) == 0;
     int Ns = 1;
     for (int s = 0; s < f.count; ++s) {
-        switch (f.r[s]) {
-            case 8: mr_stage<8, LM>(buf, twl, f.L, Ns, j, sign); break;
-            case 4: mr_stage<4, LM>(buf, twl, f.L, Ns, j, sign); break;
-            case 2: mr_stage<2, LM>(buf, twl, f.L, Ns, j, sign); break;
-            case 3: mr_stage<3, LM>(buf, twl, f.L, Ns, j, sign); break;
-            case 5: mr_stage<5, LM>(buf, twl, f.L, Ns, j, sign); break;
-            default:
-                if constexpr (R7) mr_stage<7, LM>(buf, twl, f.L, Ns, j, sign);
-                break;
-        }
+        if (even && s == 0)
+            mr_stage_r<false, LM, false, true>(f.r[s], buf, twl, f.L, Ns, j, sign);
+        else if (even && s == 1)
+            mr_stage_r<R7, LM, true, false>(f.r[s], buf, twl, f.L, Ns, j, sign);
+        else
+            mr_stage_r<R7, LM, false, false>(f.r[s], buf, twl, f.L, Ns, j, sign);
         Ns *= f.r[s];
     }
 }
@@ -707,7 +730,7 @@ constexpr int ct_ns(int L, int s) {
     return ns;
 }
 
-template <int R, int NS, int L>
+template <int R, int NS, int L, bool SWI, bool SWO>
 __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, int j, int sign) {
     constexpr int nb = L / R, step = L / (NS * R), kB = (nb + 63) / 64;
     double2 v[kB][R];
@@ -718,7 +741,7 @@ __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, in
             const int k = b % NS;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                double2 x = buf[b + q * nb];
+                double2 x = buf[lds_ix<SWI>(b + q * nb, L & ~7)];
                 if (q > 0 && NS > 1) {
                     const double2 w = twl[q * k * step];
                     x = cmul(x, sign < 0 ? w : make_double2(w.x, -w.y));
@@ -736,7 +759,7 @@ __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, in
             const int k = b % NS;
             const int d = (b - k) * R + k;
 #pragma unroll
-            for (int q = 0; q < R; ++q) buf[d + q * NS] = v[i][q];
+            for (int q = 0; q < R; ++q) buf[lds_ix<SWO>(d + q * NS, L & ~7)] = v[i][q];
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -745,7 +768,8 @@ __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, in
 template <int L, int S>
 __device__ __forceinline__ void fft_ct_stages(double2* buf, const double2* twl, int j, int sign) {
     if constexpr (ct_radix(L, S) != 0) {
-        mr_stage_ct<ct_radix(L, S), ct_ns(L, S), L>(buf, twl, j, sign);
+        constexpr bool sw = L % 2 == 0;  // swizzled between the first two stages (lds_ix)
+        mr_stage_ct<ct_radix(L, S), ct_ns(L, S), L, sw && S == 1, sw && S == 0>(buf, twl, j, sign);
         fft_ct_stages<L, S + 1>(buf, twl, j, sign);
     }
 }
@@ -793,8 +817,17 @@ __device__ __forceinline__ void stage_table(double2* dst, const double2* __restr
 }
 
 
+// LDS column stride of passes A / C with tc columns per block: N1 padded to the residue that keeps
+// the tile's transposing stores (a ds_write_b128 group of 8 lanes spans 8 columns for tc = 8) and
+// the loads that read it back free of bank conflicts: 7 mod 16 for tc = 8, 4 mod 8 for 4, 8 mod 16
+// for 2 (an enumeration over the usual N1 on the banking model of MI355X_MICROARCH.md's LDS table).
+__host__ __device__ inline int mr_col_stride(int N1, int tc) {
+    const int t = tc >= 8 ? 7 : (tc == 4 ? 4 : 8), m = tc == 4 ? 8 : 16;
+    return N1 + ((t - N1) % m + m) % m;
+}
+
 // Pass A: forward column FFTs of length N1 (one wave per column, tc = waves per block), * W_n^(n2 k1),
-// stored transposed S[k1 N2 + n2].  LDS: tile tc x N1, W_N1 (N1), W_n^r (N2).  Mode 0 batches past
+// stored transposed S[k1 N2 + n2].  LDS: tile tc x sc (mr_col_stride), W_N1 (N1), W_n^r (N2).  Mode 0 batches past
 // the block pairs (batch = n_pairs + c) are the IR channels c: their columns go to H, so the IR
 // spectra's column pass rides in the same launch as the audio's.
 template <int MODE, bool R7, int LM, int L1>
@@ -806,8 +839,8 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     const int64_t batch = blockIdx.y;
     const bool ir = MODE == 1 || (MODE == 0 && batch >= a.n_pairs);
     const int64_t ch = MODE == 1 ? batch : batch - a.n_pairs;
-    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
-    double2* twl = lds + (size_t)tc * N1;
+    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc, sc = mr_col_stride(N1, tc);
+    double2* twl = lds + (size_t)tc * sc;
     double2* tr = twl + N1;
     double2 v[IT];
 #pragma unroll
@@ -837,10 +870,10 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), n1 = i >> lgc;
-        if (n1 < N1) lds[(size_t)c * N1 + n1] = v[it];
+        if (n1 < N1) lds[(size_t)c * sc + n1] = v[it];
     }
     __syncthreads();
-    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, -1);
+    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
     double2* dst = ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
     // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r; this thread's column n2 is fixed and k1 steps
@@ -852,7 +885,7 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int k1 = k10 + 64 * it;
-        if (k1 < N1 && n2 < N2) dst[(int64_t)k1 * N2 + n2] = cmul(lds[(size_t)c * N1 + k1], cmul(twl[q], tr[r]));
+        if (k1 < N1 && n2 < N2) dst[(int64_t)k1 * N2 + n2] = cmul(lds[(size_t)c * sc + k1], cmul(twl[q], tr[r]));
         q += dq;
         r += dr;
         if (r >= N2) {
@@ -937,7 +970,7 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
 }
 
 // Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
-// blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x N1, W_N1 (N1).
+// blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x sc, W_N1 (N1).
 template <bool R7, int LM, int L1>
 __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     constexpr int IT = LM / 64;
@@ -946,9 +979,9 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
     const int64_t pair = blockIdx.y >> 1;
     const int ch = blockIdx.y & 1;
-    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc;
+    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc, sc = mr_col_stride(N1, tc);
     const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
-    double2* twl = lds + (size_t)tc * N1;
+    double2* twl = lds + (size_t)tc * sc;
     double2 v[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -961,10 +994,10 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     for (int it = 0; it < IT; ++it) {
         const int i = threadIdx.x + it * nt;
         const int c = i & (tc - 1), k1 = i >> lgc;
-        if (k1 < N1) lds[(size_t)c * N1 + k1] = v[it];
+        if (k1 < N1) lds[(size_t)c * sc + k1] = v[it];
     }
     __syncthreads();
-    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * N1, twl, m.f1, threadIdx.x & 63, +1);
+    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, +1);
     __syncthreads();
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
     if (m.fuse2) {
@@ -983,7 +1016,7 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
             const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
             if (n1 < half && n2 < N2) {
                 const int64_t idx = (int64_t)N2 * n1 + n2;
-                const double2 lo = lds[(size_t)c * N1 + n1], hi = lds[(size_t)c * N1 + n1 + half];
+                const double2 lo = lds[(size_t)c * sc + n1], hi = lds[(size_t)c * sc + n1 + half];
                 const bool odd = b1 < a.n_blocks;  // the pair's second block exists
                 const int64_t t = b1 * sr + idx;
                 if (t < a.len) {
@@ -1006,7 +1039,7 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
         const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
         if (n1 < N1 && n2 < N2) {
             const int64_t idx = (int64_t)N2 * n1 + n2;
-            const double2 x = lds[(size_t)c * N1 + n1];
+            const double2 x = lds[(size_t)c * sc + n1];
             if (b0 < a.n_blocks) y0[idx] = x.x;
             if (b1 < a.n_blocks) y1[idx] = x.y;
         }
@@ -1188,8 +1221,10 @@ static MrArgs mr_args(const ConvPlan* p, const PassArgs& a) {
 // batched block pairs, 2 for the two IR channels and the single live block, for more blocks);
 // pass B one wave per row, `rows` rows per block.
 static unsigned mr_tiles(const ConvPlan* p, int tc) { return (unsigned)((p->N2 + tc - 1) / tc); }
-static size_t mr_lds_a(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1 + p->N2) * sizeof(double2); }
-static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * p->N1 + p->N1) * sizeof(double2); }
+static size_t mr_lds_a(const ConvPlan* p, int tc) {
+    return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1 + p->N2) * sizeof(double2);
+}
+static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
 template <int MODE, bool R7, int LM, int L2>
