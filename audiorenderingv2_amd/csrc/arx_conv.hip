@@ -774,6 +774,72 @@ __device__ __forceinline__ void fft_ct_stages(double2* buf, const double2* twl, 
     }
 }
 
+// mr_stage_ct over two independent buffers at once (pass B's two inverse row FFTs): the same
+// indices and twiddles, twice the independent work between a lane's LDS round trips.
+template <int R, int NS, int L, bool SWI, bool SWO>
+__device__ __forceinline__ void mr_stage_ct2(double2* buf0, double2* buf1, const double2* twl, int j, int sign) {
+    constexpr int nb = L / R, step = L / (NS * R), kB = (nb + 63) / 64;
+    double2 v[kB][R], u[kB][R];
+#pragma unroll
+    for (int i = 0; i < kB; ++i) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
+            const int k = b % NS;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                double2 x = buf0[lds_ix<SWI>(b + q * nb, L & ~7)];
+                double2 y = buf1[lds_ix<SWI>(b + q * nb, L & ~7)];
+                if (q > 0 && NS > 1) {
+                    const double2 w = twl[q * k * step];
+                    const double2 ws = sign < 0 ? w : make_double2(w.x, -w.y);
+                    x = cmul(x, ws);
+                    y = cmul(y, ws);
+                }
+                v[i][q] = x;
+                u[i][q] = y;
+            }
+            dft_radix<R>(v[i], sign);
+            dft_radix<R>(u[i], sign);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < kB; ++i) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
+            const int k = b % NS;
+            const int d = (b - k) * R + k;
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                buf0[lds_ix<SWO>(d + q * NS, L & ~7)] = v[i][q];
+                buf1[lds_ix<SWO>(d + q * NS, L & ~7)] = u[i][q];
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int L, int S>
+__device__ __forceinline__ void fft_ct_stages2(double2* buf0, double2* buf1, const double2* twl, int j, int sign) {
+    if constexpr (ct_radix(L, S) != 0) {
+        constexpr bool sw = L % 2 == 0;
+        mr_stage_ct2<ct_radix(L, S), ct_ns(L, S), L, sw && S == 1, sw && S == 0>(buf0, buf1, twl, j, sign);
+        fft_ct_stages2<L, S + 1>(buf0, buf1, twl, j, sign);
+    }
+}
+
+// Two in-place FFTs of the same length by one wave (interleaved for a compile-time plan).
+template <bool R7, int LM, int L>
+__device__ __forceinline__ void fft2_wave_any(double2* buf0, double2* buf1, const double2* twl, const Factors& f, int j,
+                                              int sign) {
+    if constexpr (L > 0) {
+        fft_ct_stages2<L, 0>(buf0, buf1, twl, j, sign);
+    } else {
+        fft_mr_wave<R7, LM>(buf0, twl, f, j, sign);
+        fft_mr_wave<R7, LM>(buf1, twl, f, j, sign);
+    }
+}
+
 // In-place FFT of one row / column by one wave: the compile-time plan when L > 0, else the
 // run-time plan f (R7 / LM: see fft_mr_wave).
 template <bool R7, int LM, int L>
@@ -794,7 +860,7 @@ struct MrArgs {
     PassArgs p;
     Factors f1, f2;  // the column (N1) and row (N2) sub-FFTs
     int32_t batches;  // pass B: batches in its 1-D grid
-    int32_t fuse2;    // pass C: n == 2 sr and N1 even -- write the pair's odd output segment directly
+    int32_t chain;    // pass_c_chain: pairs per block
 };
 
 
@@ -920,7 +986,11 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
     // every global operand of the row up front: the row, H_0 and H_1's rows and the four-step
     // twiddles, so the wave's only global round trip before its stores is this one
-    double2 v[IT], h[IT], h1[IT], tw[IT];
+    // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r (as in pass A): two small tables that stay in
+    // L2, where the direct W_n^(n2 k1) gathered lines from all of the n-entry table
+    double2 v[IT], h[IT], h1[IT], twq[IT], twr[IT];
+    const int step = 64 * k1, dq = step / N2, dr = step - dq * N2;
+    int q = (j * k1) / N2, r = j * k1 - q * N2;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
         const int i = j + 64 * it;
@@ -929,7 +999,14 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
         v[it] = in ? row[i] : make_double2(0.0, 0.0);
         h[it] = in0 ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
         h1[it] = in0 ? a.H[(size_t)a.M + (int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
-        tw[it] = in0 ? a.tw[(int64_t)i * k1] : make_double2(1.0, 0.0);  // W_n^(n2 k1), n2 k1 < n
+        twq[it] = in0 ? a.tw[(int64_t)q * N2] : make_double2(1.0, 0.0);
+        twr[it] = in0 ? a.tw[r] : make_double2(1.0, 0.0);
+        q += dq;
+        r += dr;
+        if (r >= N2) {
+            r -= N2;
+            ++q;
+        }
     }
     stage_table<IT>(tw2, a.tw, N2, N1, nt);  // W_N2^i = W_n^(i N1)
 #pragma unroll
@@ -951,21 +1028,30 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
         }
         return;
     }
-    for (int c = 0; c < 2; ++c) {
+    // both channels' products (spec x H_0 -> work, spec x H_1 -> spec), then both inverse row FFTs
+    // interleaved
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            if (i < N2) work[i] = cmul(spec[i], c == 0 ? work[i] : h1[it]);
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            const double2 x = spec[i];
+            work[i] = cmul(x, work[i]);
+            spec[i] = cmul(x, h1[it]);
         }
-        __builtin_amdgcn_wave_barrier();
-        fft_wave_any<R7, LM, L2>(work, tw2, m.f2, j, +1);
-        double2* dst = a.S + ((size_t)batch * 3 + 1 + c) * a.M + (int64_t)k1 * N2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    fft2_wave_any<R7, LM, L2>(work, spec, tw2, m.f2, j, +1);
+    double2* dst0 = a.S + ((size_t)batch * 3 + 1) * a.M + (int64_t)k1 * N2;
+    double2* dst1 = dst0 + a.M;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            if (i < N2) dst[i] = cmul(work[i], make_double2(tw[it].x, -tw[it].y));
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            const double2 w = cmul(twq[it], twr[it]);
+            const double2 t = make_double2(w.x, -w.y);
+            dst0[i] = cmul(work[i], t);
+            dst1[i] = cmul(spec[i], t);
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1000,37 +1086,6 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, +1);
     __syncthreads();
     const int64_t b0 = 2 * pair, b1 = 2 * pair + 1;
-    if (m.fuse2) {
-        // n = 2 sr, N1 even: rows n1 < N1/2 hold the first half of each block's window (i = idx < sr),
-        // rows n1 + N1/2 the second.  Output segment 2p+1 = y_2p[i + sr] + y_2p+1[i] lies inside this
-        // pair: it is written here, summed in pass D's order and rounded once.  Segment 2p needs
-        // y_2p[i] (E_p) and the previous pair's y_2p-1[i + sr] (F_p-1): pass_d2.
-        const int half = N1 >> 1;
-        const int64_t sr = a.sr;
-        float* out = ch == 0 ? a.out_l : a.out_r;
-        double* E = a.Y + (pair * 2 + ch) * 2 * sr;
-        double* F = E + sr;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = threadIdx.x + it * nt;
-            const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
-            if (n1 < half && n2 < N2) {
-                const int64_t idx = (int64_t)N2 * n1 + n2;
-                const double2 lo = lds[(size_t)c * sc + n1], hi = lds[(size_t)c * sc + n1 + half];
-                const bool odd = b1 < a.n_blocks;  // the pair's second block exists
-                const int64_t t = b1 * sr + idx;
-                if (t < a.len) {
-                    double acc = 0.0;
-                    acc += hi.x;
-                    if (odd) acc += lo.y;
-                    out[t] = (float)(acc * a.scale);
-                }
-                E[idx] = lo.x;
-                F[idx] = odd ? hi.y : 0.0;
-            }
-        }
-        return;
-    }
     double* y0 = a.Y + (b0 * 2 + ch) * a.ylen;
     double* y1 = a.Y + (b1 * 2 + ch) * a.ylen;
 #pragma unroll
@@ -1046,21 +1101,99 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
     }
 }
 
-// Pass D for the fused n = 2 sr case: the even output segments 2p = F_p-1 + E_p (pass D's order),
-// and zeros past the last window; the odd segments 2p+1 were written by pass_c_mr.
-__global__ __launch_bounds__(kThreads) void pass_d2(PassArgs a) {
-    const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (t >= a.len) return;
-    const int ch = blockIdx.y;
-    const int64_t sr = a.sr, seg = t / sr, i = t - seg * sr;
-    if ((seg & 1) && seg < 2 * a.n_pairs) return;  // written by pass C
-    double acc = 0.0;
-    if (!(seg & 1)) {
-        const int64_t p = seg >> 1;
-        if (p >= 1 && 2 * p - 1 < a.n_blocks) acc += a.Y[((p - 1) * 2 + ch) * 2 * sr + sr + i];  // F_p-1
-        if (p < a.n_pairs) acc += a.Y[(p * 2 + ch) * 2 * sr + i];                               // E_p
+// Pass C for n = 2 sr and N1 even, fused with the seam sum: a block runs one column tile of one
+// channel through a chain of consecutive pairs p0 .. p1-1 (m.chain per block), preceded by pair
+// p0-1 again when p0 > 0.  Rows n1 < N1/2 of a pair's inverse columns hold the first half of each
+// block's window (i = idx < sr), rows n1 + N1/2 the second: the pair's odd output segment 2p+1 =
+// y_2p[i + sr] + y_2p+1[i] (hi.x + lo.y) lies inside the pair, and the even segment 2p =
+// y_2p-1[i + sr] + y_2p[i] adds the previous pair's hi.y, which this thread computed for the same
+// (column, row) one step earlier and holds in registers.  Sums in pass D's order (0 + F + E),
+// rounded once; no block window goes through HBM (Y), and no seam pass runs.
+template <bool R7, int LM, int L1>
+__global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
+    constexpr int IT = LM / 64;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const PassArgs& a = m.p;
+    const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2, half = N1 >> 1;
+    const int ch = blockIdx.y & 1;
+    const int64_t p0 = (int64_t)(blockIdx.y >> 1) * m.chain;
+    const int64_t p1 = p0 + m.chain < a.n_pairs ? p0 + m.chain : a.n_pairs;
+    const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc, sc = mr_col_stride(N1, tc);
+    double2* twl = lds + (size_t)tc * sc;
+    const int64_t sr = a.sr;
+    float* out = ch == 0 ? a.out_l : a.out_r;
+    stage_table<IT>(twl, a.tw, N1, N2, nt);
+    double2 v[IT];
+    double fprev[IT];  // hi.y of the previous pair at this thread's (column, row) slots
+    const int64_t pstart = p0 > 0 ? p0 - 1 : 0;
+    auto load = [&](int64_t pair) {
+        const double2* src = a.S + ((size_t)pair * 3 + 1 + ch) * a.M;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = threadIdx.x + it * nt;
+            const int c = i & (tc - 1), k1 = i >> lgc, n2 = n2_0 + c;
+            v[it] = (k1 < N1 && n2 < N2) ? src[(int64_t)k1 * N2 + n2] : make_double2(0.0, 0.0);
+        }
+    };
+    load(pstart);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) fprev[it] = 0.0;
+    for (int64_t pair = pstart; pair < p1; ++pair) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = threadIdx.x + it * nt;
+            const int c = i & (tc - 1), k1 = i >> lgc;
+            if (k1 < N1) lds[(size_t)c * sc + k1] = v[it];
+        }
+        __syncthreads();
+        if (pair + 1 < p1) load(pair + 1);  // in flight during this pair's FFT
+        fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, +1);
+        __syncthreads();
+        const int64_t b1 = 2 * pair + 1;
+        const bool odd = b1 < a.n_blocks;  // the pair's second block exists
+        const bool emit = pair >= p0;     // pair p0 - 1 only supplies fprev
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = threadIdx.x + it * nt;
+            const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
+            if (n1 < half && n2 < N2) {
+                const int64_t idx = (int64_t)N2 * n1 + n2;
+                const double2 lo = lds[(size_t)c * sc + n1], hi = lds[(size_t)c * sc + n1 + half];
+                if (emit) {
+                    const int64_t te = 2 * pair * sr + idx, to = b1 * sr + idx;
+                    if (te < a.len) {
+                        double acc = 0.0;
+                        acc += fprev[it];  // F_p-1 (zero for p = 0)
+                        acc += lo.x;       // E_p
+                        out[te] = (float)(acc * a.scale);
+                    }
+                    if (to < a.len) {
+                        double acc = 0.0;
+                        acc += hi.x;
+                        if (odd) acc += lo.y;
+                        out[to] = (float)(acc * a.scale);
+                    }
+                }
+                fprev[it] = odd ? hi.y : 0.0;
+            }
+        }
+        __syncthreads();  // the tile is rewritten by the next pair
     }
-    (ch == 0 ? a.out_l : a.out_r)[t] = (float)(acc * a.scale);
+    if (p1 == a.n_pairs) {  // the segment after the last pair: F_last alone
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = threadIdx.x + it * nt;
+            const int c = i & (tc - 1), n1 = i >> lgc, n2 = n2_0 + c;
+            if (n1 < half && n2 < N2) {
+                const int64_t idx = (int64_t)N2 * n1 + n2, t = 2 * p1 * sr + idx;
+                if (t < a.len) {
+                    double acc = 0.0;
+                    acc += fprev[it];
+                    out[t] = (float)(acc * a.scale);
+                }
+            }
+        }
+    }
 }
 
 int ilog2(int64_t v) {
@@ -1214,7 +1347,7 @@ static MrArgs mr_args(const ConvPlan* p, const PassArgs& a) {
     m.f1 = p->f1;
     m.f2 = p->f2;
     m.batches = 1;
-    m.fuse2 = 0;
+    m.chain = 1;
     return m;
 }
 // Direct-path launch shapes: passes A / C run one wave per column, tc columns per block (8 for the
@@ -1255,6 +1388,9 @@ static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
 #ifndef ARX_CONV_ROWSB
 #define ARX_CONV_ROWSB 4
 #endif
+#ifndef ARX_CONV_CHAIN
+#define ARX_CONV_CHAIN 2
+#endif
 template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
@@ -1262,14 +1398,16 @@ static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool wi
                        dim3(64 * ARX_CONV_TCA), mr_lds_a(p, ARX_CONV_TCA), s, m);
     if (with_ir) launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
     launch_b_mr<0, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
-    m.fuse2 = p->n == 2 * p->sr && p->N1 % 2 == 0;
+    if (p->n == 2 * p->sr && p->N1 % 2 == 0) {  // inverse columns and seams in one pass
+        m.chain = ARX_CONV_CHAIN;
+        const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
+        hipLaunchKernelGGL((pass_c_chain<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains), dim3(64 * ARX_CONV_TCC),
+                           mr_lds_c(p, ARX_CONV_TCC), s, m);
+        return;
+    }
     hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), (unsigned)(2 * pairs)),
                        dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
-    const dim3 grid_d((unsigned)((a.len + kThreads - 1) / kThreads), 2);
-    if (m.fuse2)
-        hipLaunchKernelGGL(pass_d2, grid_d, dim3(kThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL(pass_d, grid_d, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(pass_d, dim3((unsigned)((a.len + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
 }
 
 template <bool R7, int LM, int L1, int L2>
