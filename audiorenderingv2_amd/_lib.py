@@ -118,6 +118,7 @@ SIGNATURES = {
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
     "arx_trace_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "arx_conv_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_stream_create": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
     "arx_stream_destroy": (None, [_P]),
     "arx_stream_reset": (C.c_int, [_P]),

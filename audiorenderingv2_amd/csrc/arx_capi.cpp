@@ -394,6 +394,22 @@ arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out)
     return ARX_OK;
 }
 
+arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
+    if (!r || (n > 0 && !ms)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    const uint64_t have = std::min<uint64_t>(r->conv_launches, (uint64_t)arx_renderer::kTraceRing);
+    const uint64_t k = std::min<uint64_t>(have, (uint64_t)n);
+    for (uint64_t i = 0; i < k; ++i) {  // oldest of the last k first
+        const int slot = (int)((r->conv_launches - k + i) % arx_renderer::kTraceRing);
+        ARX_HIP(hipEventSynchronize(r->cev1[slot]));
+        float f = 0.f;
+        ARX_HIP(hipEventElapsedTime(&f, r->cev0[slot], r->cev1[slot]));
+        ms[i] = f;
+    }
+    if (n_out) *n_out = (size_t)k;
+    return ARX_OK;
+}
+
 const char* arx_status_string(arx_status s) {
     switch (s) {
         case ARX_OK: return "ok";
@@ -465,7 +481,6 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     };
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&r->cev0)) != hipSuccess || (e = hipEventCreate(&r->cev1)) != hipSuccess ||
         (e = hipEventCreate(&r->lev0)) != hipSuccess || (e = hipEventCreate(&r->lev1)) != hipSuccess ||
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
@@ -474,7 +489,8 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
     for (int i = 0; i < arx_renderer::kTraceRing; ++i)
-        if ((e = hipEventCreate(&r->tev0[i])) != hipSuccess || (e = hipEventCreate(&r->tev1[i])) != hipSuccess)
+        if ((e = hipEventCreate(&r->tev0[i])) != hipSuccess || (e = hipEventCreate(&r->tev1[i])) != hipSuccess ||
+            (e = hipEventCreate(&r->cev0[i])) != hipSuccess || (e = hipEventCreate(&r->cev1[i])) != hipSuccess)
             return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
@@ -510,8 +526,10 @@ void arx_destroy(arx_renderer* r) {
     for (int i = 0; i < arx_renderer::kTraceRing; ++i) {
         if (r->tev0[i]) hipEventDestroy(r->tev0[i]);
         if (r->tev1[i]) hipEventDestroy(r->tev1[i]);
+        if (r->cev0[i]) hipEventDestroy(r->cev0[i]);
+        if (r->cev1[i]) hipEventDestroy(r->cev1[i]);
     }
-    for (hipEvent_t ev : {r->cev0, r->cev1, r->lev0, r->lev1})
+    for (hipEvent_t ev : {r->lev0, r->lev1})
         if (ev) hipEventDestroy(ev);
     if (r->own_stream) hipStreamDestroy(r->own_stream);
     delete r;
@@ -774,7 +792,9 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     double tms = 0.0;
     if (last_trace_ms(r, false, &tms) == ARX_OK) r->stats.trace_ms = tms;
     float cms = 0.f;
-    if (r->conv_launches > 0 && hipEventElapsedTime(&cms, r->cev0, r->cev1) == hipSuccess) r->stats.conv_ms = cms;
+    const int cslot = (int)((r->conv_launches + arx_renderer::kTraceRing - 1) % arx_renderer::kTraceRing);
+    if (r->conv_launches > 0 && hipEventElapsedTime(&cms, r->cev0[cslot], r->cev1[cslot]) == hipSuccess)
+        r->stats.conv_ms = cms;
     *out = r->stats;
     if (r->h_counters[6]) return fail(ARX_ERR_INTERNAL, "receiver refit: a box left the quantization grid");
     return ARX_OK;
@@ -875,11 +895,12 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     arx_status st = ensure_conv(r, false);
     if (st != ARX_OK) return st;
     const bool ir_new = r->conv_ir_dirty;
-    ARX_HIP(hipEventRecord(r->cev0, r->stream));
+    const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
+    ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
     ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
                      ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
     r->conv_ir_dirty = false;
-    ARX_HIP(hipEventRecord(r->cev1, r->stream));
+    ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
     ++r->conv_launches;
     return ARX_OK;
 }
@@ -914,7 +935,8 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
     ARX_HIP(hipEventSynchronize(p1));
     float ms = 0.f;
     if (conv_ms) {
-        ARX_HIP(hipEventElapsedTime(&ms, r->cev0, r->cev1));
+        const int slot = (int)((r->conv_launches - 1) % arx_renderer::kTraceRing);
+        ARX_HIP(hipEventElapsedTime(&ms, r->cev0[slot], r->cev1[slot]));
         *conv_ms = ms;
     }
     if (proc_ms) {

@@ -57,7 +57,7 @@ struct arx_renderer {
     static constexpr int kTraceRing = 64;
     hipEvent_t tev0[kTraceRing] = {}, tev1[kTraceRing] = {};
     uint64_t trace_launches = 0;
-    hipEvent_t cev0 = nullptr, cev1 = nullptr;  // file convolution
+    hipEvent_t cev0[kTraceRing] = {}, cev1[kTraceRing] = {};  // the same around file convolutions
     uint64_t conv_launches = 0;
     hipEvent_t lev0 = nullptr, lev1 = nullptr;  // live convolution
 

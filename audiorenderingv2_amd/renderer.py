@@ -213,6 +213,13 @@ class AudioRenderer:
         check(lib().arx_trace_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
         return out[:k.value]
 
+    def conv_times(self, n: int = 64) -> np.ndarray:
+        """Device ms of the last min(n, 64) file convolutions, oldest first (arx_conv_times)."""
+        out = np.zeros(n, np.float64)
+        k = C.c_size_t()
+        check(lib().arx_conv_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
+        return out[:k.value]
+
     def stats(self) -> dict:
         s = ArxStats()
         check(lib().arx_get_stats(self._h, C.byref(s)))

@@ -138,6 +138,9 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
  * first, into ms[0..*n_out); synchronises on them.  The reference's timed window (Time taken by
  * Optix, AudioRenderer.cpp:495-518), kept per launch so a benchmark can average a timed region. */
 arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
+/* The same for the last min(n, 64) file convolutions (arx_convolute_device / _audio_file; the
+ * reference's "Time taken just to convolute", AudioRenderer.cpp:688-696). */
+arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 /* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */

@@ -404,6 +404,9 @@ def test_convolution_device_api_equals_host_api():
     import audiorenderingv2_amd._lib as L_
     L_.check(L_.lib().arx_copy_ir(r.handle, None, None, r.ir_length))  # syncs the renderer stream
     assert np.array_equal(dl.cpu().numpy(), L) and np.array_equal(dr.cpu().numpy(), R)
+    # one timing pair per convolution, host and device entry points alike (arx_conv_times)
+    t = r.conv_times(8)
+    assert len(t) == 2 and np.all(t > 0)
 
 
 def test_rejects_absorption_and_hrtf_outside_unit_interval():

@@ -33,7 +33,7 @@ for _ in range(n):
     r.set_ir(*irs)
     r.convolute_device(dx.data_ptr(), x.size, dl.data_ptr(), dr.data_ptr())
     torch.cuda.synchronize()
-    ms.append(r.stats()["conv_ms"])
+    ms.append(r.conv_times(1)[0])
 print(f"conv {np.median(ms[1:] if n > 1 else ms) * 1e3:.1f} us (median of {max(n - 1, 1)}) "
       f"checksum {float(dl.double().abs().sum() + dr.double().abs().sum()):.9e} "
       f"lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}", flush=True)
