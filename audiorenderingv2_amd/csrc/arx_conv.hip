@@ -1479,7 +1479,9 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     }
     const int64_t pairs = (S + 1) / 2;
     const int64_t ylen = plan_ylen(p);
-    if (pairs > p->pairs_cap) {
+    // the chained pass C (mr_file) keeps the block windows on chip: no Y
+    const bool windows = !(p->direct && p->n == 2 * p->sr && p->N1 % 2 == 0);
+    if (pairs > p->pairs_cap || (windows && !p->d_Y)) {
         hipFree(p->d_S);
         hipFree(p->d_Y);
         p->d_S = nullptr;
@@ -1487,8 +1489,10 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
         p->pairs_cap = 0;
         hipError_t e = hipMalloc(&p->d_S, (size_t)pairs * 3 * p->M * sizeof(double2));
         if (e != hipSuccess) return e;
-        e = hipMalloc(&p->d_Y, (size_t)pairs * 2 * 2 * ylen * sizeof(double));
-        if (e != hipSuccess) return e;
+        if (windows) {
+            e = hipMalloc(&p->d_Y, (size_t)pairs * 2 * 2 * ylen * sizeof(double));
+            if (e != hipSuccess) return e;
+        }
         p->pairs_cap = pairs;
     }
     (void)hipGetLastError();  // report this launch's error, not a stale one
@@ -1525,7 +1529,7 @@ int32_t conv_plan_block(const ConvPlan* p) { return p ? p->sr : 0; }
 hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s) {
     if (n_in < 0 || n_in > p->sr) return hipErrorInvalidValue;
     const int64_t ylen = plan_ylen(p);
-    if (p->pairs_cap < 1) {
+    if (p->pairs_cap < 1 || !p->d_Y) {
         hipFree(p->d_S);
         hipFree(p->d_Y);
         p->d_S = nullptr;
