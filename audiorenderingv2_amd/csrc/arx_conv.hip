@@ -60,6 +60,7 @@ struct ConvPlan {
     int device = 0;
     double2* d_tw = nullptr;     // W_M^e, e in [0, M)
     double2* d_H = nullptr;      // 2 * M, transposed layout [k1][k2]
+    double2* d_G = nullptr;      // direct: M, the packed IR h_L + i h_R after pass A's columns
     double2* d_S = nullptr;      // scratch spectra: pairs_cap * 3 * M (shared + 2 channels)
     double* d_Y = nullptr;       // per block, per channel M*lin (length n + sr - 1)
     int64_t pairs_cap = 0;
@@ -327,6 +328,7 @@ struct PassArgs {
     const float* ir_r;
     double2* S;         // [pair][3][M]: 0 = forward (shared), 1/2 = per channel
     double2* H;         // [2][M]
+    double2* G;         // [M]: pass_a_mr mode 0's packed IR batch
     double* Y;          // [block][2][ylen]
     int64_t ylen;       // n + sr - 1
     float* out_l;
@@ -893,9 +895,10 @@ __host__ __device__ inline int mr_col_stride(int N1, int tc) {
 }
 
 // Pass A: forward column FFTs of length N1 (one wave per column, tc = waves per block), * W_n^(n2 k1),
-// stored transposed S[k1 N2 + n2].  LDS: tile tc x sc (mr_col_stride), W_N1 (N1), W_n^r (N2).  Mode 0 batches past
-// the block pairs (batch = n_pairs + c) are the IR channels c: their columns go to H, so the IR
-// spectra's column pass rides in the same launch as the audio's.
+// stored transposed S[k1 N2 + n2].  LDS: tile tc x sc (mr_col_stride), W_N1 (N1), W_n^r (N2).  Mode 0's
+// batch past the block pairs (batch = n_pairs) is the IR, packed h_L + i h_R: its columns go to
+// G (pass_b_pair), so the IR spectra's column pass rides in the same launch as the audio's.  Mode 1
+// (IR spectra alone): batch c = IR channel c, to H.
 template <int MODE, bool R7, int LM, int L1>
 __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     constexpr int IT = LM / 64;  // per-lane elements of a column, per-thread tile loads
@@ -916,7 +919,10 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
         const int64_t idx = (int64_t)N2 * n1 + n2;
         double2 x = make_double2(0.0, 0.0);
         if (n1 < N1 && n2 < N2) {
-            if (ir) {
+            if (MODE == 0 && ir) {
+                x.x = (double)a.ir_l[idx];
+                x.y = (double)a.ir_r[idx];
+            } else if (ir) {
                 x.x = (double)(ch == 0 ? a.ir_l : a.ir_r)[idx];
             } else if (MODE == 0) {
                 if (idx < a.sr) {
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     __syncthreads();
     fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
-    double2* dst = ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
+    double2* dst = MODE == 0 && ir ? a.G : ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
     // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r; this thread's column n2 is fixed and k1 steps
     // by 64, so (q, r) advance by (64 n2) div / mod N2 -- one division per thread, not per element
     const int c = threadIdx.x & (tc - 1), n2 = n2_0 + c;
@@ -1050,6 +1056,115 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
             const double2 w = cmul(twq[it], twr[it]);
             const double2 t = make_double2(w.x, -w.y);
             dst0[i] = cmul(work[i], t);
+            dst1[i] = cmul(spec[i], t);
+        }
+    }
+}
+
+// Pass B of a file convolution with a new IR, the IR's row FFTs folded in (no separate IR pass):
+// pass A transformed the columns of g = h_L + i h_R as one packed batch (G).  For real h_L, h_R,
+//   H_L[k] = (G[k] + conj(G[-k])) / 2,   H_R[k] = (G[k] - conj(G[-k])) / (2i),
+// and with k = k1 + N1 k2, -k lies in row k1' = N1 - k1 at column N2 - 1 - k2 (k1 != 0), or in
+// row 0 at column (N2 - k2) mod N2 (k1 = 0).  A block is the two waves of mirror rows k1, k1' of
+// one block pair (rows 0 and N1/2 are their own mirrors and share a block): each wave
+// transforms its S row and its G row (interleaved), reads its mirror's G row from LDS, and goes on
+// as pass_b_mr<0>.  Block pair 0 also stores H_L / H_R, the spectra later calls reuse.
+// LDS: 2 x N2 per wave (S's spectrum; G's row, then the product), W_N2 (N2).
+template <bool R7, int LM, int L2>
+__global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
+    constexpr int IT = LM / 64;
+    extern __shared__ __attribute__((aligned(16))) double2 lds[];
+    const PassArgs& a = m.p;
+    const int N1 = a.N1, N2 = a.N2, units = (N1 + 1) / 2;
+    const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+    const int batches = (int)m.batches;
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int u = (slot / batches) * 8 + xcd;  // mirror-row unit, dealt as pass_b_mr's row groups
+    const int64_t batch = slot % batches;
+    if (u >= units) return;  // the whole block: no barrier is reached
+    const bool self = u == 0;  // rows 0 and N1 / 2: each its own mirror
+    const int k1 = w == 0 ? u : (self ? N1 / 2 : N1 - u);
+    const bool live = !(self && w == 1 && (N1 & 1));  // odd N1: row 0 has no partner row
+    double2* spec = lds + (size_t)w * 2 * N2;
+    double2* gbuf = spec + N2;
+    double2* gmir = self ? gbuf : lds + (size_t)(w ^ 1) * 2 * N2 + N2;
+    double2* tw2 = lds + (size_t)4 * N2;
+    double2* row = a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
+    double2 v[IT], g[IT], twq[IT], twr[IT];
+    const int step = 64 * k1, dq = step / N2, dr = step - dq * N2;
+    int q = (j * k1) / N2, r = j * k1 - q * N2;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        const bool in = live && i < N2;
+        v[it] = in ? row[i] : make_double2(0.0, 0.0);
+        g[it] = in ? a.G[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
+        twq[it] = in ? a.tw[(int64_t)q * N2] : make_double2(1.0, 0.0);
+        twr[it] = in ? a.tw[r] : make_double2(1.0, 0.0);
+        q += dq;
+        r += dr;
+        if (r >= N2) {
+            r -= N2;
+            ++q;
+        }
+    }
+    stage_table<IT>(tw2, a.tw, N2, N1, 128);  // W_N2^i = W_n^(i N1)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            spec[i] = v[it];
+            gbuf[i] = g[it];
+        }
+    }
+    __syncthreads();
+    fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
+    __syncthreads();  // the mirror row's G spectrum is complete
+    double2 h0[IT], h1[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            const int mi = k1 == 0 ? (i == 0 ? 0 : N2 - i) : N2 - 1 - i;
+            const double2 x = gbuf[i], y = gmir[mi];
+            h0[it] = make_double2(0.5 * (x.x + y.x), 0.5 * (x.y - y.y));  // (G + conj(G-)) / 2
+            h1[it] = make_double2(0.5 * (x.y + y.y), -0.5 * (x.x - y.x));  // (G - conj(G-)) / 2i
+        } else {
+            h0[it] = h1[it] = make_double2(0.0, 0.0);
+        }
+    }
+    if (batch == 0 && live) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = j + 64 * it;
+            if (i < N2) {
+                a.H[(int64_t)k1 * N2 + i] = h0[it];
+                a.H[(size_t)a.M + (int64_t)k1 * N2 + i] = h1[it];
+            }
+        }
+    }
+    __syncthreads();  // every mirror read is done before gbuf is overwritten
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            const double2 x = spec[i];
+            gbuf[i] = cmul(x, h0[it]);
+            spec[i] = cmul(x, h1[it]);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    fft2_wave_any<R7, LM, L2>(gbuf, spec, tw2, m.f2, j, +1);
+    if (!live) return;
+    double2* dst0 = a.S + ((size_t)batch * 3 + 1) * a.M + (int64_t)k1 * N2;
+    double2* dst1 = dst0 + a.M;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int i = j + 64 * it;
+        if (i < N2) {
+            const double2 tw = cmul(twq[it], twr[it]);
+            const double2 t = make_double2(tw.x, -tw.y);
+            dst0[i] = cmul(gbuf[i], t);
             dst1[i] = cmul(spec[i], t);
         }
     }
@@ -1290,6 +1405,7 @@ ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char
     }
     if (hipMalloc(&p->d_tw, (size_t)p->M * sizeof(double2)) != hipSuccess ||
         hipMalloc(&p->d_H, 2 * (size_t)p->M * sizeof(double2)) != hipSuccess ||
+        (p->direct && hipMalloc(&p->d_G, (size_t)p->M * sizeof(double2)) != hipSuccess) ||
         hipMemcpy(p->d_tw, tw.data(), (size_t)p->M * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess) {
         conv_plan_destroy(p);
         return bad("device allocation failed");
@@ -1301,6 +1417,7 @@ void conv_plan_destroy(ConvPlan* p) {
     if (!p) return;
     hipFree(p->d_tw);
     hipFree(p->d_H);
+    hipFree(p->d_G);
     hipFree(p->d_S);
     hipFree(p->d_Y);
     delete p;
@@ -1337,6 +1454,7 @@ static PassArgs base_args(const ConvPlan* p) {
     a.n = p->n;
     a.sr = p->sr;
     a.H = p->d_H;
+    a.G = p->d_G;
     a.ylen = plan_ylen(p);
     return a;
 }
@@ -1360,6 +1478,12 @@ static size_t mr_lds_a(const ConvPlan* p, int tc) {
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
+template <bool R7, int LM, int L2>
+static void launch_b_pair(const ConvPlan* p, int batches, MrArgs m, hipStream_t s) {
+    const unsigned units8 = (unsigned)((p->N1 + 1) / 2 + 7) / 8 * 8;  // see pass_b_pair's XCD mapping
+    m.batches = batches;
+    hipLaunchKernelGGL((pass_b_pair<R7, LM, L2>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2), s, m);
+}
 template <int MODE, bool R7, int LM, int L2>
 static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipStream_t s) {
     const unsigned groups8 = (mr_rows(p, rows) + 7) / 8 * 8;  // see pass_b_mr's XCD mapping
@@ -1376,7 +1500,8 @@ static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
 }
 
-// File convolution; with_ir: the IR columns ride in pass A's launch as two extra batches.
+// File convolution; with_ir: the packed IR's columns ride in pass A's launch as an extra batch and
+// its rows in pass B (pass_b_pair).
 // Launch shapes (columns per block in A / C, rows per block in B); the ARX_CONV_* macros exist only
 // for design-experiment builds (build.py --exp).
 #ifndef ARX_CONV_TCA
@@ -1394,10 +1519,12 @@ static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
 template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)(pairs + (with_ir ? 2 : 0))),
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)(pairs + (with_ir ? 1 : 0))),
                        dim3(64 * ARX_CONV_TCA), mr_lds_a(p, ARX_CONV_TCA), s, m);
-    if (with_ir) launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
-    launch_b_mr<0, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
+    if (with_ir)
+        launch_b_pair<R7, LM, L2>(p, (int)pairs, m, s);
+    else
+        launch_b_mr<0, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
     if (p->n == 2 * p->sr && p->N1 % 2 == 0) {  // inverse columns and seams in one pass
         m.chain = ARX_CONV_CHAIN;
         const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
