@@ -350,7 +350,7 @@ def main(argv=None) -> int:
     counts = load_profile(os.path.join("r02", "trace_counts_c3.json"))
     td = load_profile(os.path.join("r02", "trace_td_c3.json"))
     vmem = load_profile(os.path.join("r02", "trace_vmem_ceiling.json"))
-    conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02k.json"))
+    conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02m.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
         "metric": METRIC,
@@ -404,7 +404,7 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
             "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and args.workload == "c3" else None,
             "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and args.workload == "c3" else None,
-            "traffic_source": "profiles/r02/conv_traffic_r02k.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
+            "traffic_source": "profiles/r02/conv_traffic_r02m.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
                               "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
