@@ -458,6 +458,10 @@ float arx_material_absorption(const char* name, const char* const* names, const 
     return 0.5f;
 }
 
+// The per-launch timing events only time: no system-scope fence when they are recorded (with one,
+// each marker wrote back and invalidated the caches, a few microseconds of stream time per event).
+constexpr unsigned kTimingEvent = hipEventDisableSystemFence;
+
 arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     if (!out) return fail(ARX_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
@@ -489,8 +493,10 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
     for (int i = 0; i < arx_renderer::kTraceRing; ++i)
-        if ((e = hipEventCreate(&r->tev0[i])) != hipSuccess || (e = hipEventCreate(&r->tev1[i])) != hipSuccess ||
-            (e = hipEventCreate(&r->cev0[i])) != hipSuccess || (e = hipEventCreate(&r->cev1[i])) != hipSuccess)
+        if ((e = hipEventCreateWithFlags(&r->tev0[i], kTimingEvent)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&r->tev1[i], kTimingEvent)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&r->cev0[i], kTimingEvent)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&r->cev1[i], kTimingEvent)) != hipSuccess)
             return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
@@ -643,8 +649,7 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed) {
 arx_status arx_clear_histogram(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    ARX_HIP(hipMemsetAsync(r->hist(), 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream));
-    ARX_HIP(hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream));
+    ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
     return ARX_OK;
 }
 

@@ -20,6 +20,8 @@ hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_r
                               double unit, int32_t is_mono, hipStream_t s);
 // dst[i] += src[i], i < n (int64 histogram bins).
 hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hipStream_t s);
+hipError_t launch_clear(unsigned long long* hist, uint64_t n, unsigned long long* counters, int n_counters,
+                        hipStream_t s);
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
 
 // ---- moving listener (arx_receiver.hip): transform + fixed-topology refit of the receiver ----

@@ -622,6 +622,15 @@ __global__ void hist_add_kernel(long long* __restrict__ dst, const long long* __
     if (i < n) dst[i] += src[i];
 }
 
+// Histogram and counters zeroed in one launch (arx_clear_histogram; two memsets were two
+// launches of a few microseconds each, one of them for a few dozen bytes).
+__global__ void clear_kernel(unsigned long long* __restrict__ hist, uint64_t n, unsigned long long* __restrict__ counters,
+                             int n_counters) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) hist[i] = 0ull;
+    if (i < (uint64_t)n_counters) counters[i] = 0ull;
+}
+
 // Direction pre-pass: float4(dir, 0) for rays [first, first + count).
 __global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -699,6 +708,15 @@ hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hip
     (void)hipGetLastError();
     const uint64_t g = (n + 255) / 256;
     if (g > 0) hipLaunchKernelGGL(hist_add_kernel, dim3((unsigned)g), dim3(256), 0, s, dst, src, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_clear(unsigned long long* hist, uint64_t n, unsigned long long* counters, int n_counters,
+                        hipStream_t s) {
+    (void)hipGetLastError();
+    const uint64_t m = n > (uint64_t)n_counters ? n : (uint64_t)n_counters;
+    const uint64_t g = (m + 255) / 256;
+    if (g > 0) hipLaunchKernelGGL(clear_kernel, dim3((unsigned)g), dim3(256), 0, s, hist, n, counters, n_counters);
     return hipGetLastError();
 }
 
