@@ -154,3 +154,34 @@ def test_stream_equals_compat_path_when_tails_do_not_wrap():
         acc[2 * b * block:2 * b * block + 2 * n] += po.convolute_live_block(x[b * block:(b + 1) * block], hl, hr)
     out = stream_all(block, hl, hr, x)
     assert np.abs(out - acc[:out.size]).max() <= 1e-12 * np.abs(acc).max()
+
+
+@pytest.mark.parametrize("N1,N2", [(300, 320), (315, 280), (160, 200), (45, 50)])
+def test_four_step_packed_ir_mirror_rows(N1, N2):
+    """The index algebra of pass_b_pair (arx_conv.hip), in numpy: the four-step spectrum of the
+    packed IR g = h_L + i h_R (columns of length N1 * twiddle, then rows of length N2) puts
+    X[k1 + N1 k2] at row k1, column k2; -k lies in row N1 - k1 at column N2 - 1 - k2 (row 0:
+    column -k2 mod N2), and H_L = (G + conj G-) / 2, H_R = (G - conj G-) / 2i recover both IR
+    spectra."""
+    n = N1 * N2
+    rng = np.random.default_rng(N1)
+    hl, hr = rng.standard_normal(n), rng.standard_normal(n)
+    g = (hl + 1j * hr).reshape(N1, N2)  # x[N2 n1 + n2] at [n1, n2]
+    cols = np.fft.fft(g, axis=0)  # [k1, n2]
+    k1 = np.arange(N1)[:, None]
+    n2 = np.arange(N2)[None, :]
+    cols = cols * np.exp(-2j * np.pi * k1 * n2 / n)
+    G = np.fft.fft(cols, axis=1)  # [k1, k2] = X[k1 + N1 k2]
+    ref = np.fft.fft(hl + 1j * hr)
+    kk = (k1 + N1 * np.arange(N2)[None, :])
+    assert np.allclose(G, ref[kk], atol=1e-9 * n)
+    rows = np.where(np.arange(N1) == 0, 0, N1 - np.arange(N1))
+    mir = np.empty_like(G)
+    for r in range(N1):
+        i = np.arange(N2)
+        mi = np.where(i == 0, 0, N2 - i) if r == 0 else N2 - 1 - i
+        mir[r] = G[rows[r], mi]
+    HL = (G + np.conj(mir)) / 2
+    HR = (G - np.conj(mir)) / 2j
+    assert np.allclose(HL, np.fft.fft(hl)[kk], atol=1e-9 * n)
+    assert np.allclose(HR, np.fft.fft(hr)[kk], atol=1e-9 * n)
