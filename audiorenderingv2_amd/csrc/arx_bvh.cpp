@@ -319,7 +319,7 @@ struct SpatialBuilder {
 
     SpatialSplit spatial_split(const std::vector<Ref>& refs, const Box& bounds) const {
         SpatialSplit best;
-        const int nb = prm.bins;
+        const int nb = prm.spatial_bins;
         for (int axis = 0; axis < 3; ++axis) {
             const float lo = bounds.lo[axis], hi = bounds.hi[axis];
             if (!(hi > lo)) continue;

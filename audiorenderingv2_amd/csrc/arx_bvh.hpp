@@ -24,18 +24,41 @@ struct BvhBuild {
 
 // SAH build parameters (process-wide; the defaults are the production setting, design tools
 // such as tools/bvh_stats.cpp vary them).
+// The defaults below were picked on the C3 trace (profiles/r02/ab_sah.log): 128
+// object and 128 spatial bins with a node step priced at 0.8 triangle tests run 3.2 % faster than
+// 32 / 32 / 1.0.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
+// product build takes none of these macros.
+#ifndef ARX_SAH_TRAV
+#define ARX_SAH_TRAV 0.8f
+#endif
+#ifndef ARX_SAH_LEAF_MAX
+#define ARX_SAH_LEAF_MAX 4
+#endif
+#ifndef ARX_SAH_BINS
+#define ARX_SAH_BINS 128
+#endif
+#ifndef ARX_SAH_SPATIAL_BINS
+#define ARX_SAH_SPATIAL_BINS 128
+#endif
+#ifndef ARX_SAH_SPATIAL_ALPHA
+#define ARX_SAH_SPATIAL_ALPHA 1e-3f
+#endif
+#ifndef ARX_SAH_SPATIAL_BUDGET
+#define ARX_SAH_SPATIAL_BUDGET 3.0f
+#endif
 struct BuildParams {
-    int bins = 32;           // centroid bins per axis (<= 256)
-    int leaf_max = 4;        // SAH may stop at <= leaf_max triangles (always splits above)
-    float trav_cost = 1.0f;  // SAH cost of a node step relative to ...
+    int bins = ARX_SAH_BINS;           // centroid bins per axis (<= 256)
+    int leaf_max = ARX_SAH_LEAF_MAX;  // SAH may stop at <= leaf_max triangles (always splits above)
+    float trav_cost = ARX_SAH_TRAV;   // SAH cost of a node step relative to ...
     float isect_cost = 1.0f; // ... one triangle test
     // Spatial splits (SBVH, Stich, Friedrich & Dietrich 2009): a triangle may be referenced by
     // several leaves, each bounding only its clipped part.  Tried at nodes whose best object
     // split leaves children overlapping by more than spatial_alpha of the root's area, while
     // the references stay below (1 + spatial_budget) x the triangle count.
     bool spatial = true;
-    float spatial_alpha = 1e-3f;
-    float spatial_budget = 3.0f;
+    int spatial_bins = ARX_SAH_SPATIAL_BINS;  // split planes per axis (<= 256)
+    float spatial_alpha = ARX_SAH_SPATIAL_ALPHA;
+    float spatial_budget = ARX_SAH_SPATIAL_BUDGET;
     int spatial_max_depth = 64;  // spatial splits only above this depth
     // Depth cap of the spatial builder: once depth + log2(refs / leaf_max) reaches it, nodes are
     // split at the object median of their widest centroid axis, so every leaf sits at depth <=
