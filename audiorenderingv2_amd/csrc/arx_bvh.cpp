@@ -663,72 +663,6 @@ void bfs_prefix_order(BvhBuild& b, size_t k) {
     b.root.ref = map[(size_t)b.root.ref];
 }
 
-void treelet_order(BvhBuild& b, size_t k, int line_nodes, int32_t first_global) {
-    const size_t n = b.nodes.size();
-    if (n == 0 || b.root.count != 0 || line_nodes < 1) return;
-    k = std::min(k, n);
-    std::vector<int32_t> order;
-    order.reserve(n);
-    std::vector<char> placed(n, 0);
-    auto place = [&](int32_t i) { order.push_back(i); placed[(size_t)i] = 1; };
-    place(b.root.ref);
-    for (size_t h = 0; h < order.size() && order.size() < k; ++h) {  // breadth-first prefix
-        const BvhNode& nd = b.nodes[(size_t)order[h]];
-        for (int c = 0; c < 2 && order.size() < k; ++c)
-            if (nd.d[2 + c] == 0) place(nd.d[c]);
-    }
-    auto child_area = [&](const BvhNode& nd, int c) {
-        const float* xy = c == 0 ? nd.a : nd.b;
-        const float dx = xy[1] - xy[0], dy = xy[3] - xy[2], dz = nd.c[2 * c + 1] - nd.c[2 * c];
-        return dx * dy + dy * dz + dz * dx;
-    };
-    std::vector<std::pair<float, int32_t>> roots;  // treelet roots (area, node), processed LIFO
-    for (size_t h = 0; h < order.size(); ++h) {
-        const BvhNode& nd = b.nodes[(size_t)order[h]];
-        for (int c = 1; c >= 0; --c)
-            if (nd.d[2 + c] == 0 && !placed[(size_t)nd.d[c]]) roots.push_back({child_area(nd, c), nd.d[c]});
-    }
-    std::reverse(roots.begin(), roots.end());
-    std::vector<std::pair<float, int32_t>> cand;
-    while (!roots.empty()) {
-        const int32_t t = roots.back().second;
-        roots.pop_back();
-        // fill the rest of the current cache line with t's most likely descendants (largest area)
-        const int64_t pos = (int64_t)first_global + (int64_t)order.size();
-        const int cap = line_nodes - (int)(pos % line_nodes);
-        place(t);
-        cand.clear();
-        auto add_children = [&](int32_t i) {
-            const BvhNode& nd = b.nodes[(size_t)i];
-            for (int c = 0; c < 2; ++c)
-                if (nd.d[2 + c] == 0) cand.push_back({child_area(nd, c), nd.d[c]});
-        };
-        add_children(t);
-        for (int used = 1; used < cap && !cand.empty(); ++used) {
-            size_t best = 0;
-            for (size_t j = 1; j < cand.size(); ++j)
-                if (cand[j].first > cand[best].first) best = j;
-            const int32_t i = cand[best].second;
-            cand.erase(cand.begin() + (std::ptrdiff_t)best);
-            place(i);
-            add_children(i);
-        }
-        std::sort(cand.begin(), cand.end());  // the largest remaining subtree is laid out next
-        for (const auto& c : cand) roots.push_back(c);
-    }
-    std::vector<int32_t> map(n, -1);
-    for (size_t j = 0; j < order.size(); ++j) map[(size_t)order[j]] = (int32_t)j;
-    std::vector<BvhNode> out(n);
-    for (size_t i = 0; i < n; ++i) {
-        BvhNode nd = b.nodes[i];
-        for (int c = 0; c < 2; ++c)
-            if (nd.d[2 + c] == 0) nd.d[c] = map[(size_t)nd.d[c]];
-        out[(size_t)map[i]] = nd;
-    }
-    b.nodes.swap(out);
-    b.root.ref = map[(size_t)b.root.ref];
-}
-
 bool validate_bvh(const BvhNode* nodes, size_t n_nodes, size_t n_tris, const char** why) {
     return validate_bvh_range(nodes, 0, n_nodes, n_nodes, n_tris, why);
 }

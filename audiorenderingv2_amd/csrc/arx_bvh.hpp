@@ -80,10 +80,6 @@ void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
 // indices 0..k-1 (the rest keep their order, so parents still precede their children): the
 // top levels of the scene tree share cache lines.
 void bfs_prefix_order(BvhBuild& b, size_t k);
-// The same breadth-first prefix, then the rest in cache-line treelets: each treelet root fills the
-// rest of its line_nodes-node line (node index first_global + local index) with its largest-area
-// descendants; the treelet's remaining children become the next roots, largest first.
-void treelet_order(BvhBuild& b, size_t k, int line_nodes, int32_t first_global);
 BvhNode make_node(const ChildRef& c0, const ChildRef& c1);
 ChildRef empty_child();
 // Structural check of a device-ready node array (acyclic, references in range).

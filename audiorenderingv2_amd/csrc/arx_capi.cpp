@@ -570,11 +570,7 @@ arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_a
                         (double)ab, (long long)i);
     }
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
-#if defined(ARX_NODE_ORDER) && ARX_NODE_ORDER == 1 && defined(ARX_NODE_LINE)  // design experiment (build.py --exp)
-    treelet_order(r->scene, 1023, ARX_NODE_LINE, 1);
-#else
     bfs_prefix_order(r->scene, 1023);  // the top levels of the scene tree breadth-first (node locality)
-#endif
     relocate_bvh(r->scene, 1, 0);
     r->n_scene = n;
     r->scene_set = true;
