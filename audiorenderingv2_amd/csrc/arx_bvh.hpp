@@ -25,14 +25,14 @@ struct BvhBuild {
 // SAH build parameters (process-wide; the defaults are the production setting, design tools
 // such as tools/bvh_stats.cpp vary them).
 // The defaults below were picked on the C3 trace (profiles/r02/ab_sah.log): 128
-// object and 128 spatial bins with a node step priced at 0.8 triangle tests run 3.2 % faster than
-// 32 / 32 / 1.0.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
+// object and 128 spatial bins, a node step priced at 0.8 triangle tests and leaves of at most 2
+// triangles run ≈5 % faster than 32 / 32 / 1.0 / 4.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
 // product build takes none of these macros.
 #ifndef ARX_SAH_TRAV
 #define ARX_SAH_TRAV 0.8f
 #endif
 #ifndef ARX_SAH_LEAF_MAX
-#define ARX_SAH_LEAF_MAX 4
+#define ARX_SAH_LEAF_MAX 2
 #endif
 #ifndef ARX_SAH_BINS
 #define ARX_SAH_BINS 128
