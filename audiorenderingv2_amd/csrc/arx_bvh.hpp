@@ -25,8 +25,9 @@ struct BvhBuild {
 // SAH build parameters (process-wide; the defaults are the production setting, design tools
 // such as tools/bvh_stats.cpp vary them).
 // The defaults below were picked on the C3 trace (profiles/r02/ab_sah.log): 128
-// object and 128 spatial bins, a node step priced at 0.8 triangle tests and leaves of at most 2
-// triangles run ≈5 % faster than 32 / 32 / 1.0 / 4.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
+// object and 128 spatial bins, a node step priced at 0.8 triangle tests, leaves of at most 2
+// triangles and spatial splits tried down to an overlap of 1e-5 of the root area run ≈6 % faster
+// than 32 / 32 / 1.0 / 4 / 1e-3.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
 // product build takes none of these macros.
 #ifndef ARX_SAH_TRAV
 #define ARX_SAH_TRAV 0.8f
@@ -41,7 +42,7 @@ struct BvhBuild {
 #define ARX_SAH_SPATIAL_BINS 128
 #endif
 #ifndef ARX_SAH_SPATIAL_ALPHA
-#define ARX_SAH_SPATIAL_ALPHA 1e-3f
+#define ARX_SAH_SPATIAL_ALPHA 1e-5f
 #endif
 #ifndef ARX_SAH_SPATIAL_BUDGET
 #define ARX_SAH_SPATIAL_BUDGET 3.0f
