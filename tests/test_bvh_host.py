@@ -78,3 +78,22 @@ def test_breadth_first_renumbering(checker, tmp_path, k):
     in breadth-first order, the tree still valid and closest hits still exact (k = 100000:
     the whole tree renumbered)."""
     run(checker, cylinders_scene(seed=11), tmp_path, n_rays=600, env={"BFS_K": k})
+
+
+def test_threaded_build_is_deterministic(tmp_path):
+    """The spatial builder builds the top subtrees on threads (arx_bvh.cpp SpatialBuilder::inner):
+    the node and triangle arrays must not depend on thread timing, within a process or across
+    processes, at a size where the thread path is taken (> 4096 references per subtree)."""
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "tree_hash")
+    subprocess.run([gxx, "-O2", "-std=c++17", "-pthread", "-I", CSRC, os.path.join(REPO, "tests", "cpp", "tree_hash.cpp"),
+                    os.path.join(CSRC, "arx_bvh.cpp"), "-o", exe], check=True)
+    tri_v = cylinders_scene(n_cyl=400, n_box=200, seed=11)
+    path = tmp_path / "scene.f32"
+    np.ascontiguousarray(tri_v, np.float32).tofile(path)
+    outs = [subprocess.run([exe, str(path), str(len(tri_v))], capture_output=True, text=True, check=True).stdout.split()
+            for _ in range(2)]
+    assert int(outs[0][2]) > 8 * 4096 // 4, outs  # big enough for the threaded top levels
+    assert outs[0][0] == outs[0][1] == outs[1][0] == outs[1][1], outs
