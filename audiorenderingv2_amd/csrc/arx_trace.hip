@@ -658,7 +658,10 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
 #ifndef ARX_TRACE_STEPS
 #define ARX_TRACE_STEPS 12
 #endif
-constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = 12, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
+#ifndef ARX_TRACE_LEAF_THRESH
+#define ARX_TRACE_LEAF_THRESH 12
+#endif
+constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
 constexpr int kSimdsPerCu = 4;
 
 template <bool Q16, bool GSTACK>
