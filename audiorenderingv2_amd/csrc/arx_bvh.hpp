@@ -25,12 +25,12 @@ struct BvhBuild {
 // SAH build parameters (process-wide; the defaults are the production setting, design tools
 // such as tools/bvh_stats.cpp vary them).
 // The defaults below were picked on the C3 trace (profiles/r02/ab_sah.log): 128
-// object and 128 spatial bins, a node step priced at 0.8 triangle tests, leaves of at most 2
-// triangles and spatial splits tried down to an overlap of 1e-5 of the root area run ≈6 % faster
-// than 32 / 32 / 1.0 / 4 / 1e-3.  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
+// object and 128 spatial bins, leaves of at most 2 triangles and spatial splits tried down to an
+// overlap of 1e-5 of the root area run ≈7 % faster than 32 / 32 / leaves <= 4 / 1e-3 (node step
+// priced at one triangle test: 1.1 % faster than 0.8 over three paired runs at these settings).  Design experiments (build.py --exp TAG -D ARX_SAH_TRAV=...) vary them; the
 // product build takes none of these macros.
 #ifndef ARX_SAH_TRAV
-#define ARX_SAH_TRAV 0.8f
+#define ARX_SAH_TRAV 1.0f
 #endif
 #ifndef ARX_SAH_LEAF_MAX
 #define ARX_SAH_LEAF_MAX 2
