@@ -13,6 +13,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libarx.so")  # the product library (no environment override)
 
 ARX_OK = 0
+ABI_VERSION = 2  # include/arx.h ARX_ABI_VERSION
 STATUS_NAMES = {
     0: "ARX_OK", 1: "ARX_ERR_INVALID_ARGUMENT", 2: "ARX_ERR_HIP", 3: "ARX_ERR_OUT_OF_MEMORY",
     4: "ARX_ERR_NOT_READY", 5: "ARX_ERR_IO", 6: "ARX_ERR_INTERNAL",
@@ -41,6 +42,8 @@ class ArxStats(C.Structure):
         ("trace_ms", C.c_double), ("conv_ms", C.c_double),
         ("n_scene_tris", C.c_int64), ("n_receiver_tris", C.c_int64), ("n_nodes", C.c_int64),
         ("bvh_depth", C.c_int32),
+        ("tree_hash", C.c_uint64), ("trace_vgprs", C.c_int32), ("trace_waves_per_simd", C.c_int32),
+        ("trace_waves_target", C.c_int32), ("trace_format", C.c_int32),
     ]
 
 
@@ -117,8 +120,19 @@ SIGNATURES = {
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
+    "arx_debug_node_images": (C.c_int, [_P, _P, _P, C.c_size_t, _F, C.POINTER(C.c_uint64)]),
     "arx_trace_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_conv_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "arx_live_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "arx_timing_ring": (C.c_int32, []),
+    "arx_device_count": (C.c_int32, []),
+    "arx_device_alloc": (C.c_int, [C.c_int32, C.c_size_t, C.POINTER(_P)]),
+    "arx_device_free": (None, [C.c_int32, _P]),
+    "arx_memcpy": (C.c_int, [C.c_int32, _P, _P, C.c_size_t]),
+    "arx_runtime_info": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "arx_scene_build_count": (C.c_uint64, []),
+    "arx_debug_scene_roundtrip": (C.c_int, [_F, _F, C.c_int64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "arx_group_allreduce_f64": (C.c_int, [_P, _D, C.c_size_t, C.c_int]),
     "arx_stream_create": (C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
     "arx_stream_destroy": (None, [_P]),
     "arx_stream_reset": (C.c_int, [_P]),
@@ -193,7 +207,7 @@ def lib() -> C.CDLL:
                 fn = getattr(handle, name)
                 fn.restype = res
                 fn.argtypes = args
-            if handle.arx_abi_version() != 1:
+            if handle.arx_abi_version() != ABI_VERSION:
                 raise ArxError(6, "ABI version mismatch")
             _lib = handle
         return _lib

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -119,16 +120,17 @@ arx_status prepare_receiver_model(arx_renderer* r) {
     r->recv_refit = n <= kRefitMaxTris;
     r->recv_radius = radius * 1.0001f + 1e-6f;  // |R v| = |v|: the rotated halves stay in this ball
     if (!r->recv_refit) return ARX_OK;
-    build_bvh(tv.data(), ab.data(), 0.0f, n, (int32_t)r->n_scene, r->recv);
-    relocate_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), (int32_t)r->scene.tris.size());
+    const BvhBuild& sc = r->scene_img->bvh;
+    build_bvh(tv.data(), ab.data(), 0.0f, n, (int32_t)r->scene_img->n_input, r->recv);
+    relocate_bvh(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size());
     const char* why = "";
-    const size_t total_nodes = 1 + r->scene.nodes.size() + r->recv.nodes.size();
-    const size_t total_tris = r->scene.tris.size() + r->recv.tris.size();
-    if (!validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(), total_nodes,
+    const size_t total_nodes = 1 + sc.nodes.size() + r->recv.nodes.size();
+    const size_t total_tris = sc.tris.size() + r->recv.tris.size();
+    if (!validate_bvh_range(r->recv.nodes.data(), 1 + sc.nodes.size(), r->recv.nodes.size(), total_nodes,
                             total_tris, &why))
         return fail(ARX_ERR_INTERNAL, "BVH validation failed (receiver): %s", why);
     // refit schedule: inner nodes by depth, deepest level first
-    const int32_t base = 1 + (int32_t)r->scene.nodes.size();
+    const int32_t base = 1 + (int32_t)sc.nodes.size();
     std::vector<int32_t> depth(r->recv.nodes.size(), 0);
     int32_t max_d = 0;
     for (size_t i = 0; i < r->recv.nodes.size(); ++i)  // parents precede children (pre-order)
@@ -173,14 +175,24 @@ arx_status prepare_receiver_model(arx_renderer* r) {
     return ARX_OK;
 }
 
-// World-space bound of the placed receiver (for the quantization grid): the refit path's ball, or
-// the host-built sub-tree's root box.
+// Box padding of the refit kernel (RefitArgs::pad): at least the builder's 1e-5 * max|coordinate|
+// for any vertex of the placed receiver (|v| <= |center| + radius).
+float refit_pad(const arx_renderer* r) {
+    float mx = 0.0f;
+    for (int k = 0; k < 3; ++k) mx = std::max(mx, std::fabs(r->center[k]));
+    return std::max(1e-5f * (mx + r->recv_radius) * 1.001f, 1e-6f);
+}
+
+// World-space bound of the placed receiver (for the quantization grid): the refit path's ball
+// widened by the refit kernel's box padding (the padded boxes it quantizes must stay on the grid),
+// or the host-built sub-tree's root box.
 void receiver_bound(const arx_renderer* r, float lo[3], float hi[3], bool* empty) {
     *empty = (r->recv_local[0].size() + r->recv_local[1].size()) == 0;
+    const float pad = r->recv_refit ? refit_pad(r) : 0.0f;
     for (int k = 0; k < 3; ++k) {
         if (r->recv_refit) {
-            lo[k] = r->center[k] - r->recv_radius;
-            hi[k] = r->center[k] + r->recv_radius;
+            lo[k] = r->center[k] - r->recv_radius - 2.0f * pad;
+            hi[k] = r->center[k] + r->recv_radius + 2.0f * pad;
         } else {
             lo[k] = r->recv.root.lo[k];
             hi[k] = r->recv.root.hi[k];
@@ -189,7 +201,9 @@ void receiver_bound(const arx_renderer* r, float lo[3], float hi[3], bool* empty
 }
 
 arx_status ensure_device_scene(arx_renderer* r) {
-    if (!r->scene_set) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
+    if (!r->scene_img) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
+    const SceneImage& img = *r->scene_img;
+    const BvhBuild& sc = img.bvh;
     const bool model_changed = r->recv_model_dirty || r->scene_dirty;
     if (model_changed) {
         arx_status st = prepare_receiver_model(r);
@@ -209,11 +223,11 @@ arx_status ensure_device_scene(arx_renderer* r) {
             place_vertices(loc.data(), 3 * nt, r->center[0], r->center[1], r->center[2], r->yaw, tv.data() + base);
             ab.insert(ab.end(), (size_t)nt, side == 0 ? -1.0f : -2.0f);
         }
-        build_bvh(tv.data(), ab.data(), 0.0f, (int64_t)ab.size(), (int32_t)r->n_scene, r->recv);
-        relocate_bvh(r->recv, 1 + (int32_t)r->scene.nodes.size(), (int32_t)r->scene.tris.size());
+        build_bvh(tv.data(), ab.data(), 0.0f, (int64_t)ab.size(), (int32_t)img.n_input, r->recv);
+        relocate_bvh(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size());
     }
-    const size_t n_nodes = 1 + r->scene.nodes.size() + r->recv.nodes.size();
-    const size_t n_tris = r->scene.tris.size() + r->recv.tris.size();
+    const size_t n_nodes = 1 + sc.nodes.size() + r->recv.nodes.size();
+    const size_t n_tris = sc.tris.size() + r->recv.tris.size();
     bool full = r->scene_dirty;
     if (n_nodes > r->nodes_cap) {
         if (r->d_cnodes) ARX_HIP(hipFree(r->d_cnodes));
@@ -222,10 +236,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->d_qnodes = nullptr;
         size_t cap = n_nodes + 1024;
         ARX_HIP(hipMalloc(&r->d_cnodes, cap * sizeof(BvhNode)));
-#ifndef ARX_QNODES_ALLOC_FACTOR
-#define ARX_QNODES_ALLOC_FACTOR 1  // design experiments only (build.py --exp)
-#endif
-        ARX_HIP(hipMalloc(&r->d_qnodes, ARX_QNODES_ALLOC_FACTOR * cap * sizeof(QNode2)));
+        ARX_HIP(hipMalloc(&r->d_qnodes, cap * sizeof(QNode2)));
         r->nodes_cap = cap;
         full = true;
     }
@@ -237,23 +248,24 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
-    // quantized copy: a new grid (and a full re-quantization) when the scene changed, or once
-    // when the receiver first leaves the grid (a listener walking out of the room): the new
-    // grid spans the old one, the scene, the receiver and the emitter with half the extent as
-    // margin, so such a walk re-grids once or twice, not per frame.  An emitter off the grid
-    // (checked per launch, arx_trace_rays) makes the launches take the f32 nodes instead.
+    // The quantization grid: made when the scene changes, grown when the receiver leaves it (a
+    // listener walking out of the room): the new grid spans the old one, the scene, the receiver
+    // and the emitter with half the extent as margin, so such a walk re-grids once or twice, not
+    // per frame.  Either way the quantized copy is re-made on the device from the coded nodes
+    // (launch_requant16): no host quantization, no upload, no synchronisation inside a frame.  An
+    // emitter off the grid (checked per launch, arx_trace_rays) makes that launch take the f32 nodes.
     float rlo[3], rhi[3];
     bool recv_empty = false;
     receiver_bound(r, rlo, rhi, &recv_empty);
     const bool grow = !full && r->qgrid_set && pose_changed && !recv_empty && !qgrid_contains(r->qgrid, rlo, rhi);
-    const bool requant = full || !r->qgrid_set || grow;
-    if (requant) {
+    const bool regrid = full || !r->qgrid_set || grow;
+    if (regrid) {
         float lo[3], hi[3];
         for (int k = 0; k < 3; ++k) {
             lo[k] = hi[k] = r->emitter[k];
-            if (r->scene.root.count >= 0) {
-                lo[k] = std::min(lo[k], r->scene.root.lo[k]);
-                hi[k] = std::max(hi[k], r->scene.root.hi[k]);
+            if (sc.root.count >= 0) {
+                lo[k] = std::min(lo[k], sc.root.lo[k]);
+                hi[k] = std::max(hi[k], sc.root.hi[k]);
             }
             if (!recv_empty) {
                 lo[k] = std::min(lo[k], rlo[k]);
@@ -267,104 +279,246 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->qgrid = make_qgrid(lo, hi, grow ? 0.5 : 0.1);
         r->qgrid_set = true;
     }
-    const bool recv_on_grid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
-    if (full || requant || (!r->recv_refit && pose_changed) || (r->recv_refit && model_changed)) {
-        // host uploads: the top node (its receiver child comes from the refit kernel on the refit
-        // path), the scene part when it changed, the receiver part on the host path
-        const bool host_recv = !r->recv_refit;
-        BvhNode top = make_node(r->scene.root, host_recv ? r->recv.root : empty_child());
-        {
-            const char* why = "";
-            if (full && !validate_bvh_range(r->scene.nodes.data(), 1, r->scene.nodes.size(), n_nodes, n_tris, &why))
-                return fail(ARX_ERR_INTERNAL, "BVH validation failed (scene): %s", why);
-            if ((host_recv && !validate_bvh_range(r->recv.nodes.data(), 1 + r->scene.nodes.size(), r->recv.nodes.size(),
-                                                  n_nodes, n_tris, &why)) ||
-                !validate_bvh_range(&top, 0, 1, n_nodes, n_tris, &why))
-                return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
-        }
-        // coded copies of the parts being uploaded (kept in host vectors that live until the sync)
-        BvhNode ctop;
+    const bool host_recv = !r->recv_refit;
+    const bool top_changed = full || model_changed || (host_recv && pose_changed);
+    if (full || top_changed) {
+        // host uploads, only when the scene or the receiver model changed, or on the host-receiver
+        // path: the top node (its receiver child comes from the refit kernel on the refit path),
+        // the scene's coded nodes and triangles, the receiver part on the host path
+        BvhNode top = make_node(sc.root, host_recv ? r->recv.root : empty_child());
+        const char* why = "";
+        if ((host_recv && !validate_bvh_range(r->recv.nodes.data(), 1 + sc.nodes.size(), r->recv.nodes.size(), n_nodes,
+                                              n_tris, &why)) ||
+            !validate_bvh_range(&top, 0, 1, n_nodes, n_tris, &why))
+            return fail(ARX_ERR_INTERNAL, "BVH validation failed: %s", why);
+        BvhNode ctop;  // pageable sources below live until the synchronisation at the end of this block
         code_nodes(&top, 1, &ctop);
-        std::vector<BvhNode> cscene, crecv(host_recv ? r->recv.nodes.size() : 0);
+        std::vector<BvhNode> crecv(host_recv ? r->recv.nodes.size() : 0);
         if (host_recv) code_nodes(r->recv.nodes.data(), r->recv.nodes.size(), crecv.data());
         ARX_HIP(hipMemcpyAsync(r->d_cnodes, &ctop, sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-        r->qtop_h.assign(1, QNode2{});
-        r->qrecv_h.assign(crecv.size(), QNode2{});
-        const bool q_ok = quantize_nodes16(&ctop, 1, r->qgrid, r->qtop_h.data()) &&
-                          quantize_nodes16(crecv.data(), crecv.size(), r->qgrid, r->qrecv_h.data());
-        if (q_ok) ARX_HIP(hipMemcpyAsync(r->d_qnodes, r->qtop_h.data(), sizeof(QNode2), hipMemcpyHostToDevice, r->stream));
-        if ((full || requant) && !r->scene.nodes.empty()) {
-            cscene.resize(r->scene.nodes.size());
-            code_nodes(r->scene.nodes.data(), r->scene.nodes.size(), cscene.data());
-            if (full)
-                ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, cscene.data(), cscene.size() * sizeof(BvhNode),
-                                       hipMemcpyHostToDevice, r->stream));
-            r->qscene_h.assign(cscene.size(), QNode2{});
-            if (!quantize_nodes16(cscene.data(), cscene.size(), r->qgrid, r->qscene_h.data()))
-                return fail(ARX_ERR_INTERNAL, "BVH quantization failed (scene box outside the grid)");
-            ARX_HIP(hipMemcpyAsync(r->d_qnodes + 1, r->qscene_h.data(), r->qscene_h.size() * sizeof(QNode2),
+        if (full && !img.coded.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1, img.coded.data(), img.coded.size() * sizeof(BvhNode),
                                    hipMemcpyHostToDevice, r->stream));
-        } else if (full || requant) {
-            r->qscene_h.clear();
-        }
-        if (full && !r->scene.tris.empty())
-            ARX_HIP(hipMemcpyAsync(r->d_tris, r->scene.tris.data(), r->scene.tris.size() * sizeof(TriRec),
+        if (full && !sc.tris.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_tris, sc.tris.data(), sc.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice,
+                                   r->stream));
+        if (host_recv && !crecv.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + sc.nodes.size(), crecv.data(), crecv.size() * sizeof(BvhNode),
                                    hipMemcpyHostToDevice, r->stream));
-        if (host_recv && !r->recv.nodes.empty()) {
-            ARX_HIP(hipMemcpyAsync(r->d_cnodes + 1 + r->scene.nodes.size(), crecv.data(),
-                                   crecv.size() * sizeof(BvhNode), hipMemcpyHostToDevice, r->stream));
-            if (q_ok)
-                ARX_HIP(hipMemcpyAsync(r->d_qnodes + 1 + r->scene.nodes.size(), r->qrecv_h.data(),
-                                       r->qrecv_h.size() * sizeof(QNode2), hipMemcpyHostToDevice, r->stream));
-        }
         if (host_recv && !r->recv.tris.empty())
-            ARX_HIP(hipMemcpyAsync(r->d_tris + r->scene.tris.size(), r->recv.tris.data(),
-                                   r->recv.tris.size() * sizeof(TriRec), hipMemcpyHostToDevice, r->stream));
-        r->q_valid = q_ok && recv_on_grid;
-        // the host vectors are pageable: make sure the copies are done before they can change
+            ARX_HIP(hipMemcpyAsync(r->d_tris + sc.tris.size(), r->recv.tris.data(), r->recv.tris.size() * sizeof(TriRec),
+                                   hipMemcpyHostToDevice, r->stream));
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
-    if (r->recv_refit && (pose_changed || full || requant)) {
+    if (regrid || top_changed) {
+        // the quantized copy of the top node and the scene (and the host-built receiver) from the
+        // coded nodes on the device; on the refit path the refit below writes the receiver's
+        // quantized nodes itself (its coded ones may not exist yet)
+        const size_t nq = host_recv ? n_nodes : 1 + sc.nodes.size();
+        ARX_HIP(launch_requant16(r->d_cnodes, nq, r->qgrid, r->d_qnodes,
+                                 reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
+        ++r->requants;
+    }
+    r->q_valid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
+    if (r->recv_refit && (pose_changed || full || regrid)) {
         // the listener move itself: one kernel, no host copies, no synchronisation
         RefitArgs a;
         std::memset(&a, 0, sizeof(a));
         a.local_tris = r->d_recv_local;
         a.n_tris = (int32_t)r->recv.tris.size();
-        a.tri_base = (int32_t)r->scene.tris.size();
+        a.tri_base = (int32_t)sc.tris.size();
         a.local_nodes = r->d_recv_nodes;
         a.n_nodes = (int32_t)r->recv.nodes.size();
-        a.node_base = 1 + (int32_t)r->scene.nodes.size();
+        a.node_base = 1 + (int32_t)sc.nodes.size();
         a.level_nodes = r->d_recv_levels;
         a.level_start = r->d_recv_levels + r->recv_level_count;
         a.n_levels = r->recv_levels;
         a.root_ref = r->recv.root.ref;
         a.root_count = r->recv.root.count;
         receiver_rotation(r->yaw, a.m);
-        float mx = 0.0f;
-        for (int k = 0; k < 3; ++k) {
-            a.t[k] = r->center[k];
-            mx = std::max(mx, std::fabs(r->center[k]));
-        }
-        a.pad = std::max(1e-5f * (mx + r->recv_radius) * 1.001f, 1e-6f);  // >= the builder's pad
+        for (int k = 0; k < 3; ++k) a.t[k] = r->center[k];
+        a.pad = refit_pad(r);  // >= the builder's pad; receiver_bound covers it
         a.grid = r->qgrid;
         a.tris = r->d_tris;
         a.cnodes = r->d_cnodes;
-        a.qnodes = recv_on_grid ? r->d_qnodes : nullptr;
+        a.qnodes = r->q_valid ? r->d_qnodes : nullptr;
         a.flag = reinterpret_cast<unsigned int*>(r->d_counters + 6);
         if (a.n_tris > 0) ARX_HIP(launch_receiver_refit(a, r->stream));
-        r->q_valid = r->q_valid && recv_on_grid;
     }
     r->scene_dirty = false;
     r->recv_model_dirty = false;
     r->recv_pose_dirty = false;
-    r->stats.n_scene_tris = r->n_scene;
+    r->stats.n_scene_tris = img.n_input;
     r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
     r->stats.n_nodes = (int64_t)n_nodes;
-    r->stats.bvh_depth = 1 + std::max(r->scene.depth, r->recv.depth);
+    r->stats.bvh_depth = 1 + std::max(sc.depth, r->recv.depth);
+    r->stats.tree_hash = img.hash;
     return ARX_OK;
 }
 
 }  // namespace
+
+// A streaming convolution (arx_stream_*).  It belongs to its renderer: arx_destroy releases the
+// device side of every stream still attached (r = NULL afterwards), so a stream outliving its
+// renderer fails cleanly instead of touching freed memory.
+struct arx_stream {
+    arx_renderer* r = nullptr;
+    int device = 0;
+    StreamPlan* plan = nullptr;
+    uint64_t ir_generation = ~0ull;  // the IR the partition spectra were made from
+    double* d_in = nullptr;          // host-API staging: block frames in, 2 * block out
+    double* d_out = nullptr;
+};
+
+namespace {
+void release_stream(arx_stream* s) {
+    hipSetDevice(s->device);
+    if (s->r && s->r->stream) hipStreamSynchronize(s->r->stream);
+    if (s->plan) stream_plan_destroy(s->plan);
+    hipFree(s->d_in);
+    hipFree(s->d_out);
+    s->plan = nullptr;
+    s->d_in = s->d_out = nullptr;
+    s->r = nullptr;
+}
+
+arx_status live_stream(const arx_stream* s) {
+    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    if (!s->r) return fail(ARX_ERR_NOT_READY, "the stream's renderer was destroyed");
+    return ARX_OK;
+}
+}  // namespace
+
+namespace {
+std::atomic<uint64_t> g_scene_builds{0};
+
+// 64-bit content hash (word-wise multiply / xor-shift mix; not cryptographic): identifies a built
+// tree in stored profiles (arx_stats::tree_hash).
+uint64_t hash_words(const void* p, size_t bytes, uint64_t h) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    size_t i = 0;
+    for (; i + 8 <= bytes; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, b + i, 8);
+        h ^= w * 0x9E3779B97F4A7C15ull;
+        h = (h << 27 | h >> 37) * 0xC2B2AE3D27D4EB4Full;
+    }
+    for (; i < bytes; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    return h;
+}
+
+uint64_t scene_hash(const BvhBuild& b) {
+    uint64_t h = hash_words(b.nodes.data(), b.nodes.size() * sizeof(BvhNode), 0x243F6A8885A308D3ull);
+    return hash_words(b.tris.data(), b.tris.size() * sizeof(TriRec), h);
+}
+
+// serialized scene: header, nodes, triangle records
+struct SceneHeader {
+    uint64_t magic;
+    uint64_t n_nodes, n_tris;
+    int64_t n_input;
+    uint64_t hash;
+    ChildRef root;
+    int32_t depth;
+    int32_t pad;
+};
+constexpr uint64_t kSceneMagic = 0x3145435341585241ull;  // "ARXSCE1"
+}  // namespace
+
+arx_status arx::check_scene_input(const float* tri_v, const float* tri_abs, int64_t n) {
+    if (n < 0 || (n > 0 && (!tri_v || !tri_abs))) return fail(ARX_ERR_INVALID_ARGUMENT, "bad scene arrays");
+    if (n > (int64_t)0x3fffffff) return fail(ARX_ERR_INVALID_ARGUMENT, "too many triangles");
+    for (int64_t i = 0; i < 9 * n; ++i)
+        if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
+    // absorption in [0, 1], or the receiver marks -1 / -2 (getMaterialAbsorption): the int64
+    // fixed-point histogram's headroom (arx_frac_bits) assumes a ray's energy never grows
+    for (int64_t i = 0; i < n; ++i) {
+        const float ab = tri_abs[i];
+        if (!(ab >= 0.0f && ab <= 1.0f) && ab != -1.0f && ab != -2.0f)
+            return fail(ARX_ERR_INVALID_ARGUMENT, "absorption %g of triangle %lld: must be in [0, 1] (or -1 / -2 receiver)",
+                        (double)ab, (long long)i);
+    }
+    return ARX_OK;
+}
+
+SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_t n) {
+    auto img = std::make_shared<SceneImage>();
+    build_bvh(tri_v, tri_abs, 0.5f, n, 0, img->bvh);
+    bfs_prefix_order(img->bvh, 1023);  // the top levels of the scene tree breadth-first (node locality)
+    relocate_bvh(img->bvh, 1, 0);
+    img->coded.resize(img->bvh.nodes.size());
+    code_nodes(img->bvh.nodes.data(), img->bvh.nodes.size(), img->coded.data());
+    img->n_input = n;
+    img->hash = scene_hash(img->bvh);
+    g_scene_builds.fetch_add(1);
+    return img;
+}
+
+std::vector<uint8_t> arx::serialize_scene(const SceneImage& s) {
+    SceneHeader h;
+    std::memset(&h, 0, sizeof(h));
+    h.magic = kSceneMagic;
+    h.n_nodes = s.bvh.nodes.size();
+    h.n_tris = s.bvh.tris.size();
+    h.n_input = s.n_input;
+    h.hash = s.hash;
+    h.root = s.bvh.root;
+    h.depth = s.bvh.depth;
+    const size_t nb = h.n_nodes * sizeof(BvhNode), tb = h.n_tris * sizeof(TriRec);
+    std::vector<uint8_t> out(sizeof(h) + nb + tb);
+    std::memcpy(out.data(), &h, sizeof(h));
+    if (nb) std::memcpy(out.data() + sizeof(h), s.bvh.nodes.data(), nb);
+    if (tb) std::memcpy(out.data() + sizeof(h) + nb, s.bvh.tris.data(), tb);
+    return out;
+}
+
+SceneRef arx::deserialize_scene(const uint8_t* p, size_t n, const char** why) {
+    SceneHeader h;
+    if (!p || n < sizeof(h)) {
+        *why = "short scene image";
+        return nullptr;
+    }
+    std::memcpy(&h, p, sizeof(h));
+    if (h.magic != kSceneMagic || h.n_nodes > (1ull << 31) || h.n_tris > (1ull << 31) ||
+        n != sizeof(h) + h.n_nodes * sizeof(BvhNode) + h.n_tris * sizeof(TriRec)) {
+        *why = "malformed scene image";
+        return nullptr;
+    }
+    auto img = std::make_shared<SceneImage>();
+    img->bvh.nodes.resize(h.n_nodes);
+    img->bvh.tris.resize(h.n_tris);
+    if (h.n_nodes) std::memcpy(img->bvh.nodes.data(), p + sizeof(h), h.n_nodes * sizeof(BvhNode));
+    if (h.n_tris)
+        std::memcpy(img->bvh.tris.data(), p + sizeof(h) + h.n_nodes * sizeof(BvhNode), h.n_tris * sizeof(TriRec));
+    img->bvh.root = h.root;
+    img->bvh.depth = h.depth;
+    img->n_input = h.n_input;
+    img->hash = scene_hash(img->bvh);
+    if (img->hash != h.hash) {
+        *why = "scene image hash mismatch";
+        return nullptr;
+    }
+    if (!validate_bvh_range(img->bvh.nodes.data(), 1, img->bvh.nodes.size(), 1 + img->bvh.nodes.size(),
+                            img->bvh.tris.size(), why))
+        return nullptr;
+    img->coded.resize(h.n_nodes);
+    code_nodes(img->bvh.nodes.data(), img->bvh.nodes.size(), img->coded.data());
+    return img;
+}
+
+arx_status arx::set_scene_image(arx_renderer* r, SceneRef img) {
+    const char* why = "";
+    const BvhBuild& b = img->bvh;
+    if (!validate_bvh_range(b.nodes.data(), 1, b.nodes.size(), 1 + b.nodes.size(), b.tris.size(), &why))
+        return fail(ARX_ERR_INTERNAL, "BVH validation failed (scene): %s", why);
+    r->scene_img = std::move(img);
+    r->scene_dirty = true;
+    r->recv_model_dirty = true;  // receiver ids and offsets follow the scene
+    return ARX_OK;
+}
 
 arx_status arx::last_trace_ms(arx_renderer* r, bool wait, double* ms) {
     if (r->trace_launches == 0) return fail(ARX_ERR_NOT_READY, "no trace launch yet");
@@ -378,35 +532,93 @@ arx_status arx::last_trace_ms(arx_renderer* r, bool wait, double* ms) {
 
 extern "C" {
 
-arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
+}  // extern "C"
+
+namespace {
+// Device times of the last min(n, ring) launches recorded in one of the renderer's event rings.
+arx_status ring_times(arx_renderer* r, const hipEvent_t* ev0, const hipEvent_t* ev1, uint64_t launches, double* ms,
+                      size_t n, size_t* n_out) {
     if (!r || (n > 0 && !ms)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    const uint64_t have = std::min<uint64_t>(r->trace_launches, (uint64_t)arx_renderer::kTraceRing);
+    const uint64_t have = std::min<uint64_t>(launches, (uint64_t)arx_renderer::kTraceRing);
     const uint64_t k = std::min<uint64_t>(have, (uint64_t)n);
     for (uint64_t i = 0; i < k; ++i) {  // oldest of the last k first
-        const int slot = (int)((r->trace_launches - k + i) % arx_renderer::kTraceRing);
-        ARX_HIP(hipEventSynchronize(r->tev1[slot]));
+        const int slot = (int)((launches - k + i) % arx_renderer::kTraceRing);
+        ARX_HIP(hipEventSynchronize(ev1[slot]));
         float f = 0.f;
-        ARX_HIP(hipEventElapsedTime(&f, r->tev0[slot], r->tev1[slot]));
+        ARX_HIP(hipEventElapsedTime(&f, ev0[slot], ev1[slot]));
         ms[i] = f;
     }
     if (n_out) *n_out = (size_t)k;
     return ARX_OK;
 }
+}  // namespace
+
+extern "C" {
+
+arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
+    return r ? ring_times(r, r->tev0, r->tev1, r->trace_launches, ms, n, n_out)
+             : fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+}
 
 arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
-    if (!r || (n > 0 && !ms)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
-    ARX_HIP(hipSetDevice(r->cfg.device));
-    const uint64_t have = std::min<uint64_t>(r->conv_launches, (uint64_t)arx_renderer::kTraceRing);
-    const uint64_t k = std::min<uint64_t>(have, (uint64_t)n);
-    for (uint64_t i = 0; i < k; ++i) {  // oldest of the last k first
-        const int slot = (int)((r->conv_launches - k + i) % arx_renderer::kTraceRing);
-        ARX_HIP(hipEventSynchronize(r->cev1[slot]));
-        float f = 0.f;
-        ARX_HIP(hipEventElapsedTime(&f, r->cev0[slot], r->cev1[slot]));
-        ms[i] = f;
-    }
-    if (n_out) *n_out = (size_t)k;
+    return r ? ring_times(r, r->cev0, r->cev1, r->conv_launches, ms, n, n_out)
+             : fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+}
+
+arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) {
+    return r ? ring_times(r, r->lev0, r->lev1, r->live_launches, ms, n, n_out)
+             : fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+}
+
+int32_t arx_timing_ring(void) { return arx_renderer::kTraceRing; }
+
+int32_t arx_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? (int32_t)n : -1;
+}
+
+arx_status arx_device_alloc(int32_t device, size_t bytes, void** out) {
+    if (!out) return fail(ARX_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    ARX_HIP(hipSetDevice(device));
+    ARX_HIP(hipMalloc(out, std::max<size_t>(bytes, 1)));
+    return ARX_OK;
+}
+
+void arx_device_free(int32_t device, void* p) {
+    if (!p) return;
+    hipSetDevice(device);
+    hipFree(p);
+}
+
+arx_status arx_memcpy(int32_t device, void* dst, const void* src, size_t bytes) {
+    if (bytes > 0 && (!dst || !src)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(device));
+    if (bytes > 0) ARX_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return ARX_OK;
+}
+
+uint64_t arx_scene_build_count(void) { return g_scene_builds.load(); }
+
+arx_status arx_debug_scene_roundtrip(const float* tri_v, const float* tri_abs, int64_t n, uint64_t* hash,
+                                     uint64_t* bytes) {
+    arx_status st = check_scene_input(tri_v, tri_abs, n);
+    if (st != ARX_OK) return st;
+    SceneRef a = build_scene_image(tri_v, tri_abs, n);
+    const std::vector<uint8_t> img = serialize_scene(*a);
+    const char* why = "";
+    SceneRef b = deserialize_scene(img.data(), img.size(), &why);
+    if (!b) return fail(ARX_ERR_INTERNAL, "scene image: %s", why);
+    const bool same = a->hash == b->hash && a->n_input == b->n_input && a->bvh.depth == b->bvh.depth &&
+                      a->bvh.nodes.size() == b->bvh.nodes.size() && a->bvh.tris.size() == b->bvh.tris.size() &&
+                      std::memcmp(a->bvh.nodes.data(), b->bvh.nodes.data(), a->bvh.nodes.size() * sizeof(BvhNode)) == 0 &&
+                      std::memcmp(a->bvh.tris.data(), b->bvh.tris.data(), a->bvh.tris.size() * sizeof(TriRec)) == 0 &&
+                      std::memcmp(a->coded.data(), b->coded.data(), a->coded.size() * sizeof(BvhNode)) == 0 &&
+                      std::memcmp(&a->bvh.root, &b->bvh.root, sizeof(ChildRef)) == 0;
+    if (!same) return fail(ARX_ERR_INTERNAL, "scene image round trip changed the tree");
+    if (hash) *hash = a->hash;
+    if (bytes) *bytes = img.size();
     return ARX_OK;
 }
 
@@ -485,7 +697,6 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     };
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&r->lev0)) != hipSuccess || (e = hipEventCreate(&r->lev1)) != hipSuccess ||
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long))) != hipSuccess ||
@@ -496,8 +707,14 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
         if ((e = hipEventCreateWithFlags(&r->tev0[i], kTimingEvent)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&r->tev1[i], kTimingEvent)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&r->cev0[i], kTimingEvent)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&r->cev1[i], kTimingEvent)) != hipSuccess)
+            (e = hipEventCreateWithFlags(&r->cev1[i], kTimingEvent)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&r->lev0[i], kTimingEvent)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&r->lev1[i], kTimingEvent)) != hipSuccess)
             return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
+    // the production trace kernel's register allocation, as the runtime sees it (arx_stats)
+    if ((e = trace_kernel_occupancy(true, &r->stats.trace_vgprs, &r->stats.trace_waves_per_simd,
+                                    &r->stats.trace_waves_target)) != hipSuccess)
+        return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
@@ -511,6 +728,8 @@ void arx_destroy(arx_renderer* r) {
     if (!r) return;
     hipSetDevice(r->cfg.device);
     if (r->stream) hipStreamSynchronize(r->stream);
+    for (arx_stream* s : r->streams) release_stream(s);  // the handles stay valid but detached
+    r->streams.clear();
     if (r->conv) conv_plan_destroy(r->conv);
     if (r->conv_live) conv_plan_destroy(r->conv_live);
     hipFree(r->d_live_in);
@@ -534,9 +753,9 @@ void arx_destroy(arx_renderer* r) {
         if (r->tev1[i]) hipEventDestroy(r->tev1[i]);
         if (r->cev0[i]) hipEventDestroy(r->cev0[i]);
         if (r->cev1[i]) hipEventDestroy(r->cev1[i]);
+        if (r->lev0[i]) hipEventDestroy(r->lev0[i]);
+        if (r->lev1[i]) hipEventDestroy(r->lev1[i]);
     }
-    for (hipEvent_t ev : {r->lev0, r->lev1})
-        if (ev) hipEventDestroy(ev);
     if (r->own_stream) hipStreamDestroy(r->own_stream);
     delete r;
 }
@@ -557,26 +776,11 @@ void* arx_get_stream(const arx_renderer* r) { return r ? (void*)r->stream : null
 
 arx_status arx_set_scene(arx_renderer* r, const float* tri_v, const float* tri_abs, int64_t n) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
-    if (n < 0 || (n > 0 && (!tri_v || !tri_abs))) return fail(ARX_ERR_INVALID_ARGUMENT, "bad scene arrays");
-    if (n > (int64_t)0x3fffffff) return fail(ARX_ERR_INVALID_ARGUMENT, "too many triangles");
-    for (int64_t i = 0; i < 9 * n; ++i)
-        if (!std::isfinite(tri_v[i])) return fail(ARX_ERR_INVALID_ARGUMENT, "non-finite vertex at %lld", (long long)i / 9);
-    // absorption in [0, 1], or the receiver marks -1 / -2 (getMaterialAbsorption): the int64
-    // fixed-point histogram's headroom (arx_frac_bits) assumes a ray's energy never grows
-    for (int64_t i = 0; i < n; ++i) {
-        const float ab = tri_abs[i];
-        if (!(ab >= 0.0f && ab <= 1.0f) && ab != -1.0f && ab != -2.0f)
-            return fail(ARX_ERR_INVALID_ARGUMENT, "absorption %g of triangle %lld: must be in [0, 1] (or -1 / -2 receiver)",
-                        (double)ab, (long long)i);
-    }
-    build_bvh(tri_v, tri_abs, 0.5f, n, 0, r->scene);
-    bfs_prefix_order(r->scene, 1023);  // the top levels of the scene tree breadth-first (node locality)
-    relocate_bvh(r->scene, 1, 0);
-    r->n_scene = n;
-    r->scene_set = true;
-    r->scene_dirty = true;
-    r->recv_model_dirty = true;  // receiver ids and offsets follow the scene
-    return ARX_OK;
+    const arx_status st = check_scene_input(tri_v, tri_abs, n);
+    if (st != ARX_OK) return st;
+    SceneRef img = build_scene_image(tri_v, tri_abs, n);
+    if (!img) return fail(ARX_ERR_OUT_OF_MEMORY, "scene build failed");
+    return set_scene_image(r, std::move(img));
 }
 
 arx_status arx_set_receiver_model(arx_renderer* r, int side, const float* tri_v, int64_t n) {
@@ -720,6 +924,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         a.gstack_lanes = lanes;
     }
     const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
+    r->stats.trace_format = a.qnodes ? 1 : 0;
     ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
@@ -961,9 +1166,11 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
     ARX_HIP(hipSetDevice(r->cfg.device));
     arx_status st = ensure_conv_live(r, (int32_t)std::max<size_t>(n_in, 1));
     if (st != ARX_OK) return st;
-    ARX_HIP(hipEventRecord(r->lev0, r->stream));
+    const int slot = (int)(r->live_launches % arx_renderer::kTraceRing);
+    ARX_HIP(hipEventRecord(r->lev0[slot], r->stream));
     ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
-    ARX_HIP(hipEventRecord(r->lev1, r->stream));
+    ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
+    ++r->live_launches;
     return ARX_OK;
 }
 
@@ -986,6 +1193,23 @@ arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t 
     if (st != ARX_OK) return st;
     ARX_HIP(hipMemcpyAsync(h_out, r->d_live_out, out_len * sizeof(double), hipMemcpyDeviceToHost, r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));
+    return ARX_OK;
+}
+
+arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, size_t n_nodes, float* grid,
+                                 uint64_t* requants) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n_nodes > (size_t)r->stats.n_nodes) return fail(ARX_ERR_INVALID_ARGUMENT, "only %lld nodes", (long long)r->stats.n_nodes);
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    if (cnodes && n_nodes) ARX_HIP(hipMemcpy(cnodes, r->d_cnodes, n_nodes * sizeof(BvhNode), hipMemcpyDeviceToHost));
+    if (qnodes && n_nodes) ARX_HIP(hipMemcpy(qnodes, r->d_qnodes, n_nodes * sizeof(QNode2), hipMemcpyDeviceToHost));
+    if (grid)
+        for (int k = 0; k < 3; ++k) {
+            grid[k] = r->qgrid.origin[k];
+            grid[3 + k] = r->qgrid.scale[k];
+        }
+    if (requants) *requants = r->requants;
     return ARX_OK;
 }
 
@@ -1012,14 +1236,6 @@ arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first, uint64_t coun
 // ---- streaming convolution (UPOLS, arx_conv.hip) --------------------------------------------------
 }  // extern "C"
 
-struct arx_stream {
-    arx_renderer* r = nullptr;
-    StreamPlan* plan = nullptr;
-    uint64_t ir_generation = ~0ull;  // the IR the partition spectra were made from
-    double* d_in = nullptr;          // host-API staging: block frames in, 2 * block out
-    double* d_out = nullptr;
-};
-
 extern "C" {
 
 arx_status arx_stream_create(arx_renderer* r, int32_t block_frames, arx_stream** out) {
@@ -1031,6 +1247,7 @@ arx_status arx_stream_create(arx_renderer* r, int32_t block_frames, arx_stream**
     arx_stream* s = new (std::nothrow) arx_stream();
     if (!s) return fail(ARX_ERR_OUT_OF_MEMORY, "host allocation failed");
     s->r = r;
+    s->device = r->cfg.device;
     char err[256] = {0};
     s->plan = stream_plan_create(r->ir_len, block_frames, r->cfg.device, err, sizeof(err));
     if (!s->plan) {
@@ -1039,32 +1256,36 @@ arx_status arx_stream_create(arx_renderer* r, int32_t block_frames, arx_stream**
     }
     if (hipMalloc(&s->d_in, (size_t)block_frames * sizeof(double)) != hipSuccess ||
         hipMalloc(&s->d_out, 2 * (size_t)block_frames * sizeof(double)) != hipSuccess) {
-        arx_stream_destroy(s);
+        release_stream(s);
+        delete s;
         return fail(ARX_ERR_OUT_OF_MEMORY, "stream buffers");
     }
+    r->streams.push_back(s);
     *out = s;
     return ARX_OK;
 }
 
 void arx_stream_destroy(arx_stream* s) {
     if (!s) return;
-    hipSetDevice(s->r->cfg.device);
-    hipStreamSynchronize(s->r->stream);
-    stream_plan_destroy(s->plan);
-    hipFree(s->d_in);
-    hipFree(s->d_out);
+    if (s->r) {
+        std::vector<arx_stream*>& v = s->r->streams;
+        v.erase(std::remove(v.begin(), v.end(), s), v.end());
+        release_stream(s);
+    }
     delete s;
 }
 
 arx_status arx_stream_reset(arx_stream* s) {
-    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    arx_status st = live_stream(s);
+    if (st != ARX_OK) return st;
     ARX_HIP(hipSetDevice(s->r->cfg.device));
     ARX_HIP(stream_reset(s->plan, s->r->stream));
     return ARX_OK;
 }
 
 arx_status arx_stream_info(const arx_stream* s, int32_t* block, int32_t* partitions, int32_t* fft_size) {
-    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    const arx_status st = live_stream(s);
+    if (st != ARX_OK) return st;
     if (block) *block = stream_plan_block(s->plan);
     if (partitions) *partitions = stream_plan_partitions(s->plan);
     if (fft_size) *fft_size = stream_plan_fft(s->plan);
@@ -1072,7 +1293,7 @@ arx_status arx_stream_info(const arx_stream* s, int32_t* block, int32_t* partiti
 }
 
 arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n_frames, double* d_out) {
-    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    if (const arx_status st0 = live_stream(s); st0 != ARX_OK) return st0;
     const int32_t B = stream_plan_block(s->plan);
     if (n_frames > (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "%zu frames exceed the stream block %d", n_frames, B);
     if ((n_frames > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
@@ -1082,14 +1303,16 @@ arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n
         ARX_HIP(stream_set_ir(s->plan, r->d_ir, r->d_ir + r->ir_len, r->stream));
         s->ir_generation = r->ir_generation;
     }
-    ARX_HIP(hipEventRecord(r->lev0, r->stream));
+    const int slot = (int)(r->live_launches % arx_renderer::kTraceRing);
+    ARX_HIP(hipEventRecord(r->lev0[slot], r->stream));
     ARX_HIP(stream_run(s->plan, d_in, (int64_t)n_frames, d_out, r->stream));
-    ARX_HIP(hipEventRecord(r->lev1, r->stream));
+    ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
+    ++r->live_launches;
     return ARX_OK;
 }
 
 arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames, double* h_out, size_t out_len) {
-    if (!s) return fail(ARX_ERR_INVALID_ARGUMENT, "stream is NULL");
+    if (const arx_status st0 = live_stream(s); st0 != ARX_OK) return st0;
     const int32_t B = stream_plan_block(s->plan);
     if (out_len != 2 * (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "output must hold 2*block = %d doubles", 2 * B);
     if (n_frames > (size_t)B) return fail(ARX_ERR_INVALID_ARGUMENT, "%zu frames exceed the stream block %d", n_frames, B);

@@ -14,10 +14,13 @@
 // A device listed more than once in arx_group_create (oversubscribing one GPU, e.g. to test the
 // sharding on a single-GPU box) cannot join an RCCL communicator twice; such a group sums its
 // histograms on that device instead (hist_add kernel) -- the same exact int64 sum.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -194,8 +197,63 @@ arx_renderer* arx_group_member(arx_group* g, int32_t i) {
     return g->members[i];
 }
 
+// The scene tree is built once per group (buildAccel, AudioRenderer.cpp:95-218, runs once per scene
+// in the reference too) and shared by the members; each uploads it to its own device at its next
+// trace.  In a one-GPU-per-process group, rank 0 builds and the tree's byte image goes to the other
+// ranks with one RCCL broadcast (staged through device memory on the member's stream).
 arx_status arx_group_set_scene(arx_group* g, const float* tri_v, const float* tri_abs, int64_t n) {
-    return for_all(g, [&](arx_renderer* r) { return arx_set_scene(r, tri_v, tri_abs, n); });
+    if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
+    const bool rank_path = g->n_ranks > 1 && g->members.size() == 1 && g->comms.size() == 1;
+    SceneRef img;
+    if (!rank_path || g->rank0 == 0) {
+        const arx_status st = check_scene_input(tri_v, tri_abs, n);
+        if (st != ARX_OK) return st;
+        img = build_scene_image(tri_v, tri_abs, n);
+        if (!img) return fail(ARX_ERR_OUT_OF_MEMORY, "scene build failed");
+    }
+    if (rank_path) {
+        arx_renderer* r = g->members[0];
+        ARX_HIP(hipSetDevice(r->cfg.device));
+        std::vector<uint8_t> bytes;
+        uint64_t size = 0;
+        if (g->rank0 == 0) {
+            bytes = serialize_scene(*img);
+            size = bytes.size();
+        }
+        uint64_t* d_size = nullptr;
+        uint8_t* d_buf = nullptr;
+        auto release = [&]() {
+            hipStreamSynchronize(r->stream);
+            hipFree(d_size);
+            hipFree(d_buf);
+        };
+        arx_status st = ARX_OK;
+        auto step = [&](hipError_t e, const char* what) {
+            if (st == ARX_OK && e != hipSuccess) st = fail(ARX_ERR_HIP, "scene broadcast: %s: %s", what, hipGetErrorString(e));
+        };
+        auto nstep = [&](ncclResult_t e, const char* what) {
+            if (st == ARX_OK && e != ncclSuccess) st = fail(ARX_ERR_HIP, "scene broadcast: %s: %s", what, ncclGetErrorString(e));
+        };
+        step(hipMalloc(&d_size, sizeof(uint64_t)), "hipMalloc");
+        step(hipMemcpyAsync(d_size, &size, sizeof(uint64_t), hipMemcpyHostToDevice, r->stream), "size upload");
+        nstep(ncclBroadcast(d_size, d_size, 1, ncclUint64, 0, g->comms[0], r->stream), "size");
+        step(hipMemcpyAsync(&size, d_size, sizeof(uint64_t), hipMemcpyDeviceToHost, r->stream), "size download");
+        step(hipStreamSynchronize(r->stream), "sync");
+        if (st == ARX_OK && g->rank0 != 0) bytes.resize(size);
+        step(hipMalloc(&d_buf, std::max<uint64_t>(size, 1)), "hipMalloc");
+        if (g->rank0 == 0) step(hipMemcpyAsync(d_buf, bytes.data(), size, hipMemcpyHostToDevice, r->stream), "upload");
+        nstep(ncclBroadcast(d_buf, d_buf, size, ncclUint8, 0, g->comms[0], r->stream), "tree");
+        if (g->rank0 != 0) step(hipMemcpyAsync(bytes.data(), d_buf, size, hipMemcpyDeviceToHost, r->stream), "download");
+        step(hipStreamSynchronize(r->stream), "sync");
+        release();
+        if (st != ARX_OK) return st;
+        if (g->rank0 != 0) {
+            const char* why = "";
+            img = deserialize_scene(bytes.data(), bytes.size(), &why);
+            if (!img) return fail(ARX_ERR_INTERNAL, "scene broadcast: %s", why);
+        }
+    }
+    return for_all(g, [&](arx_renderer* r) { return set_scene_image(r, img); });
 }
 arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_v, int64_t n) {
     return for_all(g, [&](arx_renderer* r) { return arx_set_receiver_model(r, side, tri_v, n); });
@@ -247,6 +305,11 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         }
         ARX_NCCL(ncclGroupEnd());
     } else if (g->device_sum) {
+        // Member 0's stream does all of it -- sum the shards into member 0's histogram, then copy the
+        // total back into every other member's -- and the others wait for that before finalising.
+        // Every access to member 0's histogram is thus ordered on member 0's own stream, so its next
+        // clear cannot overtake a copy still reading it, and member i's next clear (after its
+        // finalise, after `summed`) cannot overtake the copy writing its histogram.
         arx_renderer* r0 = g->members[0];
         ARX_HIP(hipSetDevice(r0->cfg.device));
         for (size_t i = 1; i < g->members.size(); ++i) {
@@ -255,12 +318,11 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
             ARX_HIP(hipStreamWaitEvent(r0->stream, g->traced[i], 0));
             ARX_HIP(launch_hist_add((long long*)r0->hist(), (const long long*)r->hist(), bins, r0->stream));
         }
+        for (size_t i = 1; i < g->members.size(); ++i)
+            ARX_HIP(hipMemcpyAsync(g->members[i]->hist(), r0->hist(), bins * sizeof(long long), hipMemcpyDeviceToDevice,
+                                   r0->stream));
         ARX_HIP(hipEventRecord(g->summed, r0->stream));
-        for (size_t i = 1; i < g->members.size(); ++i) {
-            arx_renderer* r = g->members[i];
-            ARX_HIP(hipStreamWaitEvent(r->stream, g->summed, 0));
-            ARX_HIP(hipMemcpyAsync(r->hist(), r0->hist(), bins * sizeof(long long), hipMemcpyDeviceToDevice, r->stream));
-        }
+        for (size_t i = 1; i < g->members.size(); ++i) ARX_HIP(hipStreamWaitEvent(g->members[i]->stream, g->summed, 0));
     }
     // 3. every member finalises the full IR
     for (arx_renderer* r : g->members) {
@@ -294,6 +356,59 @@ arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t
     return arx_copy_ir(g->members[0], h_left, h_right, ir_len);
 }
 
+arx_status arx_group_allreduce_f64(arx_group* g, double* values, size_t n, int op) {
+    if (!g || g->members.empty() || (n > 0 && !values) || (op != 0 && op != 1))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (g->comms.empty() || n == 0 || (int32_t)g->members.size() == g->n_ranks) return ARX_OK;  // one process
+    // this process's values enter through member 0; the other local members add the identity
+    std::vector<double*> bufs(g->members.size(), nullptr);
+    std::vector<double> ident(n, op == 0 ? 0.0 : -HUGE_VAL);
+    arx_status st = ARX_OK;
+    for (size_t i = 0; i < g->members.size() && st == ARX_OK; ++i) {
+        arx_renderer* r = g->members[i];
+        if (hipSetDevice(r->cfg.device) != hipSuccess || hipMalloc(&bufs[i], n * sizeof(double)) != hipSuccess ||
+            hipMemcpyAsync(bufs[i], i == 0 ? values : ident.data(), n * sizeof(double), hipMemcpyHostToDevice,
+                           r->stream) != hipSuccess)
+            st = fail(ARX_ERR_HIP, "arx_group_allreduce_f64: staging failed");
+    }
+    if (st == ARX_OK) {
+        ncclGroupStart();
+        ncclResult_t e = ncclSuccess;
+        for (size_t i = 0; i < g->members.size() && e == ncclSuccess; ++i)
+            e = ncclAllReduce(bufs[i], bufs[i], n, ncclFloat64, op == 0 ? ncclSum : ncclMax, g->comms[i],
+                              g->members[i]->stream);
+        const ncclResult_t e2 = ncclGroupEnd();
+        if (e != ncclSuccess || e2 != ncclSuccess)
+            st = fail(ARX_ERR_HIP, "ncclAllReduce(f64) failed: %s", ncclGetErrorString(e != ncclSuccess ? e : e2));
+    }
+    if (st == ARX_OK) {
+        arx_renderer* r0 = g->members[0];
+        if (hipSetDevice(r0->cfg.device) != hipSuccess ||
+            hipMemcpyAsync(values, bufs[0], n * sizeof(double), hipMemcpyDeviceToHost, r0->stream) != hipSuccess)
+            st = fail(ARX_ERR_HIP, "arx_group_allreduce_f64: download failed");
+    }
+    for (size_t i = 0; i < g->members.size(); ++i) {
+        hipSetDevice(g->members[i]->cfg.device);
+        hipStreamSynchronize(g->members[i]->stream);
+        hipFree(bufs[i]);
+    }
+    return st;
+}
+
+arx_status arx_runtime_info(char* buf, size_t len) {
+    if (!buf || len == 0) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    Dl_info hip_dl, nccl_dl;
+    const char* hip_path = dladdr(reinterpret_cast<void*>(&hipGetDeviceCount), &hip_dl) && hip_dl.dli_fname
+                               ? hip_dl.dli_fname : "?";
+    const char* nccl_path = dladdr(reinterpret_cast<void*>(&ncclGetVersion), &nccl_dl) && nccl_dl.dli_fname
+                                ? nccl_dl.dli_fname : "?";
+    int hv = 0, nv = 0;
+    hipRuntimeGetVersion(&hv);
+    ncclGetVersion(&nv);
+    std::snprintf(buf, len, "hip=%s (runtime %d) rccl=%s (version %d)", hip_path, hv, nccl_path, nv);
+    return ARX_OK;
+}
+
 arx_status arx_group_get_stats(arx_group* g, arx_stats* out) {
     if (!g || g->members.empty() || !out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
     arx_stats sum;
@@ -311,6 +426,11 @@ arx_status arx_group_get_stats(arx_group* g, arx_stats* out) {
         sum.n_receiver_tris = s.n_receiver_tris;
         sum.n_nodes = s.n_nodes;
         sum.bvh_depth = s.bvh_depth;
+        sum.tree_hash = s.tree_hash;
+        sum.trace_vgprs = s.trace_vgprs;
+        sum.trace_waves_per_simd = s.trace_waves_per_simd;
+        sum.trace_waves_target = s.trace_waves_target;
+        sum.trace_format = s.trace_format;
     }
     *out = sum;
     return ARX_OK;

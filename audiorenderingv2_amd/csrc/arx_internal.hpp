@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -37,12 +38,36 @@ inline uint64_t n_rays(const arx_config& c) {
     return (uint64_t)(int64_t)c.rays_x * (uint64_t)(int64_t)c.rays_y * (uint64_t)(int64_t)c.rays_z;
 }
 
+// The static scene as the host builds it once (buildAccel, AudioRenderer.cpp:95-218): the SBVH
+// relocated into the device layout (scene nodes from index 1, node 0 being the top node; scene
+// triangle records from 0) and its coded copy (code_nodes).  Immutable once built, shared by every
+// renderer of a group (each uploads it to its own device).
+struct SceneImage {
+    BvhBuild bvh;
+    std::vector<BvhNode> coded;
+    int64_t n_input = 0;  // triangles given to arx_set_scene (global ids 0 .. n_input-1)
+    uint64_t hash = 0;    // content hash of nodes and triangle records (profile guards)
+};
+using SceneRef = std::shared_ptr<const SceneImage>;
+
+// Input checks of arx_set_scene (finite vertices, absorption in [0, 1] or the receiver marks).
+arx_status check_scene_input(const float* tri_v, const float* tri_abs, int64_t n);
+// One host build (counted by arx_scene_build_count).
+SceneRef build_scene_image(const float* tri_v, const float* tri_abs, int64_t n);
+// Byte image of a build for the rank path's RCCL broadcast, and its inverse (NULL + why on a
+// malformed image).
+std::vector<uint8_t> serialize_scene(const SceneImage& s);
+SceneRef deserialize_scene(const uint8_t* p, size_t n, const char** why);
+
 }  // namespace arx
 
 struct arx_renderer;
+struct arx_stream;
 namespace arx {
 // Device time (ms) of the renderer's last trace launch; wait = synchronise on it first.
 arx_status last_trace_ms(arx_renderer* r, bool wait, double* ms);
+// Install a built scene (arx_set_scene's second half): uploaded at the next trace.
+arx_status set_scene_image(arx_renderer* r, SceneRef img);
 }  // namespace arx
 
 // One renderer = one device (AudioRenderer, AudioRenderer.h:16-152).
@@ -52,22 +77,23 @@ struct arx_renderer {
     int cus = 256;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
-    // timing events: a ring of (start, end) pairs around the last kTraceRing trace launches
-    // (arx_trace_times), and separate pairs for the file and the live convolution
-    static constexpr int kTraceRing = 64;
+    // timing events: rings of (start, end) pairs around the last kTraceRing trace launches
+    // (arx_trace_times), file convolutions (arx_conv_times) and live / streaming convolutions
+    // (arx_live_times)
+    static constexpr int kTraceRing = 256;
     hipEvent_t tev0[kTraceRing] = {}, tev1[kTraceRing] = {};
     uint64_t trace_launches = 0;
-    hipEvent_t cev0[kTraceRing] = {}, cev1[kTraceRing] = {};  // the same around file convolutions
+    hipEvent_t cev0[kTraceRing] = {}, cev1[kTraceRing] = {};
     uint64_t conv_launches = 0;
-    hipEvent_t lev0 = nullptr, lev1 = nullptr;  // live convolution
+    hipEvent_t lev0[kTraceRing] = {}, lev1[kTraceRing] = {};
+    uint64_t live_launches = 0;
 
     float emitter[3] = {0.f, 0.f, 0.f};
     float center[3] = {0.f, 0.f, 0.f};
     float yaw = 0.f;
 
-    // host scene
-    int64_t n_scene = 0;
-    arx::BvhBuild scene;
+    // host scene (shared with the other members of a group)
+    arx::SceneRef scene_img;
     std::vector<float> recv_local[2];
     arx::BvhBuild recv;
     bool scene_dirty = true;
@@ -87,8 +113,8 @@ struct arx_renderer {
     arx::QNode2* d_qnodes = nullptr;   // 16-bit quantized copy of d_cnodes (same indices): the default
     arx::QGrid qgrid{};
     bool qgrid_set = false;
-    bool q_valid = false;         // d_qnodes matches the tree: the receiver is on the grid
-    std::vector<arx::QNode2> qtop_h, qscene_h, qrecv_h;  // host images of the quantized parts
+    bool q_valid = false;         // d_qnodes matches the tree (re-quantized on the device, arx_receiver.hip)
+    uint64_t requants = 0;        // device re-quantizations issued (new scene or grid)
     size_t nodes_cap = 0;
     arx::TriRec* d_tris = nullptr;
     size_t tris_cap = 0;
@@ -117,6 +143,9 @@ struct arx_renderer {
     float* d_conv_out = nullptr;
     size_t conv_cap = 0;
 
+    std::vector<arx_stream*> streams;  // live streaming convolutions of this renderer (arx_stream_create)
+
+    int32_t last_format = 0;  // node format of the last trace launch (arx_stats::trace_format)
     arx_stats stats;
 };
 

@@ -23,6 +23,9 @@ hipError_t launch_hist_add(long long* dst, const long long* src, uint64_t n, hip
 hipError_t launch_clear(unsigned long long* hist, uint64_t n, unsigned long long* counters, int n_counters,
                         hipStream_t s);
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
+// Register allocation of the production trace kernel instance (hipFuncGetAttributes numRegs), the
+// waves per SIMD it admits, and the waves per SIMD the persistent grid is sized for.
+hipError_t trace_kernel_occupancy(bool q16, int* vgprs, int* waves_admitted, int* waves_target);
 
 // ---- moving listener (arx_receiver.hip): transform + fixed-topology refit of the receiver ----
 struct RefitArgs {
@@ -47,6 +50,11 @@ struct RefitArgs {
 };
 size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels);  // bytes of LDS
 hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
+// The quantized copy of nodes [0, n) re-made on the device from the coded f32 nodes for grid g
+// (quantize_nodes16's arithmetic, bit for bit): a new scene or a grown grid costs one launch and
+// no host work or upload.  flag is set if a box falls off the grid.
+hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
+                            hipStream_t s);
 
 // ---- convolution (arx_conv.hip) ----
 struct ConvPlan;  // opaque, defined in arx_conv.hip

@@ -1,4 +1,6 @@
-// arx_receiver.hip -- moving-listener update on the device.
+// arx_receiver.hip -- moving-listener update on the device, and the
+// device re-quantization of the node tree (a new scene, or the grid grown for a listener that
+// walked off it: no host work inside a frame).
 //
 // The reference re-places the receiver half-spheres on the host (place_receiver_half,
 // OptixModel.cpp:159-257) and then rebuilds the whole GAS, pipeline and SBT (reload,
@@ -27,13 +29,12 @@ __device__ __forceinline__ int32_t child_code(int32_t ref, int32_t count) {
     return count < 0 ? kEmptyChildCode : count == 0 ? ref : ~(ref * 16 + count);  // code_nodes (arx_bvh.cpp)
 }
 
-// Outward 16-bit grid index of a plane with the 0.1-step margin (quantize_nodes16, arx_bvh.cpp).
-// inv = 1 / scale (f64): the product differs from the quotient by a few f64 ulps, far inside the
-// 0.1-step margin, so the planes stay conservative.
-__device__ __forceinline__ bool quantize_axis(const QGrid& g, const double* inv, int k, float lo, float hi,
+// Outward 16-bit grid index of a plane with the 0.1-step margin: quantize_nodes16's arithmetic
+// (arx_bvh.cpp) bit for bit (IEEE f64 division), like the device re-quantization below.
+__device__ __forceinline__ bool quantize_axis(const QGrid& g, const double* /*inv*/, int k, float lo, float hi,
                                               uint32_t& word) {
-    const double l = floor(((double)lo - (double)g.origin[k]) * inv[k] - 0.1);
-    const double h = ceil(((double)hi - (double)g.origin[k]) * inv[k] + 0.1);
+    const double l = floor(((double)lo - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
+    const double h = ceil(((double)hi - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
     if (!(l >= 0.0) || !(h <= 65535.0)) return false;
     word = (uint32_t)l | ((uint32_t)h << 16);
     return true;
@@ -196,7 +197,57 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
     }
 }
 
+// One quantized child: quantize_nodes16 (arx_bvh.cpp) on the device.  The f64 division is IEEE
+// correctly rounded on gfx950 as on the host, so q is the host's q bit for bit.
+__device__ __forceinline__ bool requant_child(const QGrid& g, const float* xy, const float* z, int32_t code,
+                                              QChild& out) {
+    const float lo[3] = {xy[0], xy[2], z[0]};
+    const float hi[3] = {xy[1], xy[3], z[1]};
+    const bool empty = code == kEmptyChildCode;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uint32_t ql = 1u, qh = 0u;  // empty: the slab between planes 0 and 1 (grid corner)
+        if (!empty) {
+            const double l = floor(((double)lo[k] - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
+            const double h = ceil(((double)hi[k] - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
+            if (!(lo[k] <= hi[k]) || !(l >= 0.0) || !(h <= 65535.0)) {
+                ok = false;
+                ql = 0u;
+                qh = 65535u;  // the whole axis: still conservative
+            } else {
+                ql = (uint32_t)l;
+                qh = (uint32_t)h;
+            }
+        }
+        out.q[k] = ql | (qh << 16);
+    }
+    out.code = code;
+    return ok;
+}
+
+__global__ __launch_bounds__(256) void requant16_kernel(const BvhNode* __restrict__ coded, uint64_t n, QGrid g,
+                                                         QNode2* __restrict__ out, unsigned int* flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const BvhNode b = coded[i];
+    QNode2 q;
+    const bool ok0 = requant_child(g, b.a, b.c, b.d[0], q.c[0]);
+    const bool ok1 = requant_child(g, b.b, b.c + 2, b.d[1], q.c[1]);
+    out[i] = q;
+    if (!(ok0 && ok1)) atomicOr(flag, 1u);
+}
+
 }  // namespace
+
+hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
+                            hipStream_t s) {
+    (void)hipGetLastError();
+    if (n == 0) return hipSuccess;
+    if (!coded || !out || !flag) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(requant16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, coded, n, g, out, flag);
+    return hipGetLastError();
+}
 
 size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels) {
     return ((((size_t)9 * n_tris + (size_t)6 * n_nodes + 3) & ~(size_t)3) + (size_t)5 * n_nodes + (size_t)n_levels + 1) *

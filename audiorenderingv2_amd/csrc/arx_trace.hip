@@ -698,6 +698,22 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_g
     return gstack ? launch<false, true>(a, cus, s) : launch<false, false>(a, cus, s);
 }
 
+hipError_t trace_kernel_occupancy(bool q16, int* vgprs, int* waves_admitted, int* waves_target) {
+    hipFuncAttributes fa;
+    const hipError_t e =
+        q16 ? hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
+                                            trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, true, false>))
+            : hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
+                                            trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, false, false>));
+    if (e != hipSuccess) return e;
+    // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    *vgprs = fa.numRegs;
+    *waves_admitted = alloc > 0 ? std::min(8, 512 / alloc) : 8;
+    *waves_target = kWaves;
+    return hipSuccess;
+}
+
 hipError_t launch_finalize_ir(const long long* hist, float* ir_left, float* ir_right, int32_t ir_len, double unit,
                               int32_t is_mono, hipStream_t s) {
     (void)hipGetLastError();

@@ -8,6 +8,7 @@ call goes through libarx.so's C ABI (include/arx.h); there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 import os
 import time
 from dataclasses import dataclass
@@ -172,6 +173,18 @@ class AudioRenderer:
         global-memory traversal stack; 0 = automatic."""
         check(lib().arx_debug_set_trace_path(self.handle, int(path)))
 
+    def node_images(self) -> dict:
+        """Parity hook (arx_debug_node_images): the device's coded f32 nodes (n x 16 words), their
+        device-made 16-bit quantized copy (n x 8 words), the grid and the re-quantization count."""
+        n = int(self.stats()["n_nodes"])
+        cn = np.empty((n, 16), np.uint32)
+        qn = np.empty((n, 8), np.uint32)
+        grid = np.empty(6, np.float32)
+        rq = C.c_uint64()
+        check(lib().arx_debug_node_images(self._h, cn.ctypes.data_as(C.c_void_p), qn.ctypes.data_as(C.c_void_p), n,
+                                          fptr(grid), C.byref(rq)))
+        return {"cnodes": cn, "qnodes": qn, "origin": grid[:3], "scale": grid[3:], "requants": int(rq.value)}
+
     def clear_histogram(self) -> None:
         check(lib().arx_clear_histogram(self._h))
 
@@ -207,17 +220,24 @@ class AudioRenderer:
         check(lib().arx_set_ir(self._h, fptr(L), fptr(R), L.size))
 
     def trace_times(self, n: int = 64) -> np.ndarray:
-        """Device ms of the last min(n, 64) trace launches, oldest first (arx_trace_times)."""
+        """Device ms of the last min(n, ring) trace launches, oldest first (arx_trace_times)."""
         out = np.zeros(n, np.float64)
         k = C.c_size_t()
         check(lib().arx_trace_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
         return out[:k.value]
 
     def conv_times(self, n: int = 64) -> np.ndarray:
-        """Device ms of the last min(n, 64) file convolutions, oldest first (arx_conv_times)."""
+        """Device ms of the last min(n, ring) file convolutions, oldest first (arx_conv_times)."""
         out = np.zeros(n, np.float64)
         k = C.c_size_t()
         check(lib().arx_conv_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
+        return out[:k.value]
+
+    def live_times(self, n: int = 64) -> np.ndarray:
+        """Device ms of the last min(n, ring) live / streaming convolution blocks (arx_live_times)."""
+        out = np.zeros(n, np.float64)
+        k = C.c_size_t()
+        check(lib().arx_live_times(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), n, C.byref(k)))
         return out[:k.value]
 
     def stats(self) -> dict:
@@ -338,8 +358,12 @@ class RenderGroup:
             arr = (C.c_int32 * len(devs))(*devs)
             check(lib().arx_group_create(C.byref(cfg), arr, len(devs), C.byref(self._g)))
         self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
-        self.members = [AudioRenderer(settings, _borrowed=C.c_void_p(lib().arx_group_member(self._g, i)))
-                        for i in range(lib().arx_group_members(self._g))]
+        self.members = []
+        for i in range(lib().arx_group_members(self._g)):
+            h = C.c_void_p(lib().arx_group_member(self._g, i))
+            cfg = ArxConfig()
+            check(lib().arx_get_config(h, C.byref(cfg)))
+            self.members.append(AudioRenderer(dataclasses.replace(settings, device=int(cfg.device)), _borrowed=h))
         if receiver is not None:
             self.set_receiver_model(*receiver)
         if scene is not None:
@@ -436,6 +460,67 @@ class RenderGroup:
         s = ArxStats()
         check(lib().arx_group_get_stats(self._g, C.byref(s)))
         return {k: getattr(s, k) for k, _ in ArxStats._fields_}
+
+    def allreduce(self, values, op: str = "sum") -> np.ndarray:
+        """This process's values combined over every process of the group (one RCCL all-reduce,
+        synchronising: also a barrier); a group living in one process returns them unchanged."""
+        v = np.ascontiguousarray(np.atleast_1d(values), np.float64).copy()
+        check(lib().arx_group_allreduce_f64(self._g, v.ctypes.data_as(C.POINTER(C.c_double)), v.size,
+                                            {"sum": 0, "max": 1}[op]))
+        return v
+
+
+class DeviceBuffer:
+    """Device memory allocated through libarx (arx_device_alloc), so that a caller such as
+    bench.py needs no other GPU framework (and libarx runs on the HIP runtime it was built with)."""
+
+    def __init__(self, device: int, nbytes: int):
+        self.device = int(device)
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(lib().arx_device_alloc(self.device, self.nbytes, C.byref(p)))
+        self.ptr = int(p.value)
+
+    @classmethod
+    def from_numpy(cls, device: int, a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(device, a.nbytes)
+        check(lib().arx_memcpy(b.device, C.c_void_p(b.ptr), a.ctypes.data_as(C.c_void_p), a.nbytes))
+        return b
+
+    def to_numpy(self, dtype, count: int | None = None) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else int(count)
+        out = np.empty(n, dt)
+        check(lib().arx_memcpy(self.device, out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes))
+        return out
+
+    def close(self) -> None:
+        if self.ptr:
+            lib().arx_device_free(self.device, C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (arx_device_count)."""
+    return int(lib().arx_device_count())
+
+
+def runtime_info() -> str:
+    """Paths and versions of the HIP and RCCL runtimes libarx resolved (arx_runtime_info)."""
+    buf = C.create_string_buffer(2048)
+    check(lib().arx_runtime_info(buf, len(buf)))
+    return buf.value.decode()
+
+
+def scene_build_count() -> int:
+    return int(lib().arx_scene_build_count())
 
 
 def place_receiver_vertices(local_xyz: np.ndarray, pos, yaw_deg: float) -> np.ndarray:

@@ -4,26 +4,37 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-One step = one pass of the hot path on every rank (BASELINE.json configs[2], per GPU):
-  trace this rank's 1M-ray shard x 16 bounces (fused HIP kernel) -> one RCCL all-reduce (int64
+One step = one pass of the hot path on every GPU (BASELINE.json configs[2], per GPU):
+  trace this GPU's 1M-ray shard x 16 bounces (fused HIP kernel) -> one RCCL all-reduce (int64
   SUM) of the 2 x 96000-bin histogram -> finalize the stereo f32 IR (libarx's native group API,
   arx_group_render) -> IR spectra + file-mode FFT convolution of A_Clapper_Board.wav channel 0
-  (807 498 frames, 48 kHz).
-The group is native: a one-GPU RCCL communicator (ncclCommInitAll) for N = 1, one
-ncclCommInitRank rank per process under torchrun (the RCCL unique id is shared once through
-torch.distributed, which otherwise only carries the barrier and the max-over-ranks timing).
+  (807 498 frames, 48 kHz) on every GPU.
+
+How the N GPUs are driven (plan_ranks):
+  * plain `python bench.py --gpus N`: ONE process drives N GPUs through one native group
+    (arx_group_create over devices 0..N-1 -> ncclCommInitAll), the design of SURVEY.md §5 / §8e;
+  * under torch.distributed.run (WORLD_SIZE = N > 1): one GPU per process (LOCAL_RANK), joined
+    with ncclCommInitRank; rank 0's RCCL unique id reaches the other ranks through a file keyed by
+    the launcher's process id and port (all ranks share one node), and barriers / max-over-ranks
+    timing are RCCL all-reduces of the group itself (arx_group_allreduce_f64).
+The process imports no other GPU framework: device buffers, streams and timing events come from
+libarx (arx_device_alloc, the renderer's own stream and per-launch event rings), so libarx runs on
+the /opt/rocm HIP / RCCL runtime it was built and tested against (`runtime` in the JSON line).
+Asking for more GPUs than the box has fails loudly instead of printing a smaller line.
 Inputs are resident in HBM before timing.  Rank 0 prints ONE JSON line.
-Scaling is weak: every rank owns 1M rays of a W*1M-ray launch (energy normalised by the total
+Scaling is weak: every GPU owns 1M rays of an N*1M-ray launch (energy normalised by the total
 count, devicePrograms.cu:208) and convolves its own copy of the stream.
 """
 from __future__ import annotations
 
 import argparse
 import contextlib
+import hashlib
 import json
 import math
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -43,10 +54,10 @@ WORKLOADS = {
     "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento",
                desc="configs[1]: conference stand-in, 100K rays x 8 bounces per GPU, 16 kHz IR, "
                     "convolution of experimento_entrada_16KHz.wav (128000 frames) per GPU"),
-    # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the ranks (strong)
+    # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the GPUs (strong)
     "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, audio="clapper", total=True,
                desc="configs[3]: conference stand-in, 10M rays x 32 bounces in total, ray-sharded across the "
-                    "ranks, 48 kHz IR, RCCL IR all-reduce; convolution of A_Clapper_Board.wav ch0 per GPU"),
+                    "GPUs, 48 kHz IR, RCCL IR all-reduce; convolution of A_Clapper_Board.wav ch0 per GPU"),
 }
 
 
@@ -56,8 +67,84 @@ def bytes_per_bounce(n_tris: int) -> int:
 
 
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
+NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2"}  # arx_stats.trace_format
 
 
+# ----------------------------------------------------------------------------- rank plumbing ---
+def plan_ranks(gpus: int, env: dict, process_group: bool = False) -> dict:
+    """--gpus N and the launcher's environment -> how this process takes part.
+
+    mode "local": this process drives devices 0..N-1 itself (one native group, ncclCommInitAll);
+    mode "rank": torch.distributed.run started one process per GPU (WORLD_SIZE > 1, or
+    --process-group at one rank): this process is rank RANK of WORLD_SIZE on device LOCAL_RANK
+    (ncclCommInitRank).  `world` is the GPU count of the whole job either way."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1 (got {gpus})")
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world > 1 or process_group:
+        if gpus not in (1, world) or (world == 1 and gpus != 1):
+            raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} processes "
+                             "(one GPU per process: pass --gpus WORLD_SIZE)")
+        rank, local = int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+        if not (0 <= rank < world) or local < 0:
+            raise ValueError(f"bad RANK={rank} / LOCAL_RANK={local} for WORLD_SIZE={world}")
+        return {"mode": "rank", "world": world, "rank": rank, "devices": [local], "local_gpus_needed": local + 1}
+    return {"mode": "local", "world": gpus, "rank": 0, "devices": list(range(gpus)), "local_gpus_needed": gpus}
+
+
+def uid_path(env: dict) -> str:
+    """Where rank 0 leaves the RCCL unique id for the other ranks of this launch: keyed by the
+    launcher (the ranks' common parent process), its rendezvous port and run id, so a file left by
+    another launch is never read."""
+    key = f"{os.getppid()}:{env.get('MASTER_ADDR', '')}:{env.get('MASTER_PORT', '')}:{env.get('TORCHELASTIC_RUN_ID', '')}"
+    return os.path.join(tempfile.gettempdir(), "arx_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16] + ".bin")
+
+
+def share_unique_id(rank: int, world: int, env: dict, make_uid, timeout_s: float = 300.0) -> bytes | None:
+    """Rank 0's RCCL unique id to every rank (a one-rank group needs none)."""
+    if world == 1:
+        return None
+    path = uid_path(env)
+    if rank == 0:
+        uid = make_uid()
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as fh:
+            fh.write(uid)
+        os.replace(tmp, path)
+        return uid
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout_s:
+        try:
+            with open(path, "rb") as fh:
+                uid = fh.read()
+            if len(uid) == 128:
+                return uid
+        except FileNotFoundError:
+            pass
+        time.sleep(0.05)
+    raise SystemExit(f"rank {rank}: no RCCL unique id from rank 0 at {path} after {timeout_s:.0f} s")
+
+
+class Ranks:
+    """Barrier / max / sum over the job's processes: RCCL all-reduces of the group itself (one
+    process driving every GPU needs none)."""
+
+    def __init__(self, group, mode: str):
+        self.g = group
+        self.multi = mode == "rank" and group.n_ranks > 1
+
+    def barrier(self) -> None:
+        if self.multi:
+            self.g.allreduce([0.0])
+
+    def max(self, v: float) -> float:
+        return float(self.g.allreduce([v], "max")[0]) if self.multi else float(v)
+
+    def sum(self, v: float) -> float:
+        return float(self.g.allreduce([v], "sum")[0]) if self.multi else float(v)
+
+
+# ------------------------------------------------------------------------------ CPU baseline ---
 def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> dict:
     """The CPU oracle (naive C ray loop + median-split BVH) on this host, bounded samples of the
     same launch: one thread, and every core this process may run on (sched_getaffinity)."""
@@ -135,36 +222,38 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def moving_listener(g, D, dev, frames: int, rays_per_rank: int) -> dict:
+# ------------------------------------------------------------------------------- extra legs ---
+def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int) -> dict:
     """the listener moves 0.05 m/frame along +x with yaw += 1 deg/frame.
     Frame latency = host wall time of: receiver re-placement (receiver sub-tree only, no scene
-    rebuild) -> trace this rank's shard -> RCCL all-reduce -> finalize IR -> new IR spectra for
-    the file and the live convolution paths, synchronised.  The reference instead re-places the
-    receiver and rebuilds the whole GAS and pipeline (OptixModel.cpp:153-257,
-    AudioRenderer.cpp:466-486, 790-798).  p50/p99 are max over ranks."""
+    rebuild; a grid that grows is re-quantized on the device) -> trace every GPU's shard -> RCCL
+    all-reduce -> finalize IR -> new IR spectra for the file and the live convolution paths on every
+    GPU, synchronised.  The reference instead re-places the receiver and rebuilds the whole GAS
+    and pipeline (OptixModel.cpp:153-257, AudioRenderer.cpp:466-486, 790-798).  p50/p99/max are
+    max over ranks."""
     from audiorenderingv2_amd.scene import CONFERENCE_LISTENER
 
     x0, y0, z0 = CONFERENCE_LISTENER
-    m = g.member(0)
     lat = []
     for k in range(frames + 3):
         g.synchronize()
         t0 = time.perf_counter()
         g.setSphereCenterInOptix((x0 + 0.05 * k, y0, z0), float(k % 360))
         g.render(timed=False)
-        m.prepare_ir_spectra(file=True, live=True)
+        for m in g.members:
+            m.prepare_ir_spectra(file=True, live=True)
         g.synchronize()
         if k >= 3:  # first frames warm the receiver rebuild path
             lat.append((time.perf_counter() - t0) * 1e3)
     a = np.array(lat)
-    return {"frames": frames, "rays_per_rank": rays_per_rank, "p50_ms": D.max_over_ranks(float(np.percentile(a, 50)), dev),
-            "p99_ms": D.max_over_ranks(float(np.percentile(a, 99)), dev),
-            "max_ms": D.max_over_ranks(float(a.max()), dev), "budget_ms": 1000.0 / 60.0,
+    return {"frames": frames, "rays_per_gpu": rays_per_gpu, "p50_ms": ranks.max(float(np.percentile(a, 50))),
+            "p99_ms": ranks.max(float(np.percentile(a, 99))), "max_ms": ranks.max(float(a.max())),
+            "budget_ms": 1000.0 / 60.0, "walk_m": 0.05 * (frames + 2),
             "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + all-reduce + finalize + IR spectra"}
 
 
 def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: int) -> dict:
-    """C5's per-rank frame on 8 GPUs: 1M rays per frame split 8 ways is 125K rays per rank.  One
+    """C5's per-GPU frame on 8 GPUs: 1M rays per frame split 8 ways is 125K rays per GPU.  One
     renderer traces rays [0, shard) of the 1M launch per frame (plus re-placement, finalize and
     IR spectra); the 8-GPU all-reduce of 768 kB adds ~10-20 us over xGMI."""
     from audiorenderingv2_amd import AudioRenderer
@@ -186,50 +275,67 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
             lat.append((time.perf_counter() - t0) * 1e3)
     r.close()
     a = np.array(lat)
-    return {"frames": frames, "rays_per_rank": shard, "p50_ms": float(np.percentile(a, 50)),
+    return {"frames": frames, "rays_per_gpu": shard, "p50_ms": float(np.percentile(a, 50)),
             "p99_ms": float(np.percentile(a, 99)), "max_ms": float(a.max()), "budget_ms": 1000.0 / 60.0,
-            "per_frame": "one rank's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra "
+            "per_frame": "one GPU's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra "
                          "(projected 8-GPU rank; the all-reduce is not included)"}
 
 
-def streaming_leg(r, audio, block: int, dev) -> dict:
+def streaming_leg(m, audio, block: int) -> dict:
     """C3's streaming overlap-add leg: the same audio fed through the streaming convolution
     (arx_stream_*: uniformly partitioned overlap-save, f64) in 4096-frame blocks, device-resident
-    (arx_stream_process_device): per-block device latency and frames/s."""
-    import torch
+    (arx_stream_process_device): per-block device latency (the renderer's live event ring) and
+    frames/s (host clock around the back-to-back blocks)."""
+    from audiorenderingv2_amd import DeviceBuffer, LiveStream
 
-    from audiorenderingv2_amd import LiveStream
-
-    s = LiveStream(r, block)
-    x = torch.from_numpy(audio.astype(np.float64)).to(dev)
+    dev = m.settings.device
+    s = LiveStream(m, block)
+    x = DeviceBuffer.from_numpy(dev, audio.astype(np.float64))
+    out = DeviceBuffer(dev, 2 * block * 8)
     nb = audio.size // block
-    out = torch.empty(2 * block, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
     for b in range(8):  # warm-up
-        s.process_device(x[b * block:].data_ptr(), block, out.data_ptr())
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(nb + 1)]
-    torch.cuda.synchronize(dev)
-    ev[0].record(stream)
+        s.process_device(x.ptr + 8 * b * block, block, out.ptr)
+    m.stats()  # synchronises the renderer's stream
+    t0 = time.perf_counter()
     for b in range(nb):
-        s.process_device(x[b * block:].data_ptr(), block, out.data_ptr())
-        ev[b + 1].record(stream)
-    torch.cuda.synchronize(dev)
-    per = np.array([ev[b].elapsed_time(ev[b + 1]) for b in range(nb)])
-    total_ms = ev[0].elapsed_time(ev[nb])
+        s.process_device(x.ptr + 8 * b * block, block, out.ptr)
+    m.stats()
+    total_s = time.perf_counter() - t0
+    per = m.live_times(nb)
     s.close()
+    x.close()
+    out.close()
     return {"block_frames": block, "blocks": nb, "partitions": s.partitions, "fft_size": s.fft_size,
-            "frames_per_s": nb * block / (total_ms * 1e-3), "block_p50_ms": float(np.percentile(per, 50)),
-            "block_p99_ms": float(np.percentile(per, 99)),
-            "block_period_ms": 1e3 * block / 48000.0,
-            "method": "device-resident, back-to-back blocks on the renderer stream, HIP events per block"}
+            "frames_per_s": nb * block / total_s, "block_p50_ms": float(np.percentile(per, 50)),
+            "block_p99_ms": float(np.percentile(per, 99)), "block_period_ms": 1e3 * block / 48000.0,
+            "method": "device-resident, back-to-back blocks on the renderer stream; per-block HIP events "
+                      "(arx_live_times), frames/s on the host clock around all blocks"}
 
 
+# -------------------------------------------------------------------------- stored profiles ---
 def load_profile(name: str) -> dict | None:
     path = os.path.join(REPO, "profiles", name)
     if os.path.exists(path):
         with open(path) as fh:
             return json.load(fh)
     return None
+
+
+def profile_guard(prof: dict | None, workload: str, stats: dict,
+                  keys: tuple = ("workload", "tree_hash", "trace_vgprs")) -> tuple[dict | None, str]:
+    """A stored PMC-derived profile applies to this run only if it was taken on the same workload,
+    the same scene tree (content hash) and the same trace kernel build (register allocation): the
+    counters cannot be read inside this run, and a stale file must not pass as a measurement.
+    (Per-query lane counts come from a separate counting build: they are guarded by the tree only.)"""
+    if prof is None:
+        return None, "missing"
+    want = {"workload": workload, "tree_hash": f"{int(stats['tree_hash']):016x}",
+            "trace_vgprs": int(stats["trace_vgprs"])}
+    want = {k: want[k] for k in keys}
+    bad = [k for k, v in want.items() if prof.get(k) != v]
+    if bad:
+        return None, "stale: " + ", ".join(f"{k} {prof.get(k)!r} != {want[k]!r}" for k in bad)
+    return prof, "matches " + " / ".join(keys)
 
 
 @contextlib.contextmanager
@@ -246,6 +352,7 @@ def _stdout_to_stderr():
         os.close(saved)
 
 
+# -------------------------------------------------------------------------------------- main ---
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,98 +365,117 @@ def main(argv=None) -> int:
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
     ap.add_argument("--process-group", action="store_true",
-                    help="join a torch.distributed group and take the one-GPU-per-process (RCCL rank) path even "
-                         "at one rank: a rehearsal of the N > 1 path on a one-GPU box")
+                    help="take the one-GPU-per-process (RCCL rank) path even at one rank: a rehearsal of the "
+                         "torch.distributed.run path on a one-GPU box")
     args = ap.parse_args(argv)
+    try:
+        plan = plan_ranks(args.gpus, os.environ, args.process_group)
+    except ValueError as e:
+        raise SystemExit(f"bench.py: {e}")
 
-    import torch
-
-    from audiorenderingv2_amd import RenderGroup, RenderSettings, conference_standin, receiver_local
-    from audiorenderingv2_amd import distributed as D
+    from audiorenderingv2_amd import (RenderGroup, RenderSettings, conference_standin, device_count, receiver_local,
+                                      runtime_info)
+    from audiorenderingv2_amd._lib import lib
+    from audiorenderingv2_amd.renderer import DeviceBuffer
     from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, reference_audio
 
-    with _stdout_to_stderr():  # an eager RCCL init prints its version banner on stdout
-        rank, world, local = D.init(force=args.process_group)
-    import torch.distributed as dist
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU (HIP); there is no CPU fallback")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ring = int(lib().arx_timing_ring())
+    if args.steps < 1 or args.steps > ring:
+        raise SystemExit(f"bench.py: --steps must be in [1, {ring}] (the renderer's per-launch timing ring)")
+    have = device_count()
+    if have < plan["local_gpus_needed"]:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {plan['local_gpus_needed']} visible GPU(s) in this "
+                         f"process, the HIP runtime sees {have}; refusing to print a line for fewer GPUs")
+    world, rank = plan["world"], plan["rank"]
     wl = WORKLOADS[args.workload]
     rx, ry, rz = wl["rays"]
-    if wl.get("total"):  # a fixed total split over the ranks (strong scaling)
+    if wl.get("total"):  # a fixed total split over the GPUs (strong scaling)
         total_rays = rx * ry * rz
         launch = (rx, ry, rz)
-    else:  # a fixed shard per rank (weak scaling)
+    else:  # a fixed shard per GPU (weak scaling)
         total_rays = rx * ry * rz * world
         launch = (rx * world, ry, rz)
     settings = RenderSettings(rays=launch, ir_length_in_seconds=2, sample_rate=wl["sample_rate"],
                               base_power=3.62, max_bounces=wl["max_bounces"], hrtf_absorption_rate=1.0, seed=1,
-                              device=local)
+                              device=plan["devices"][0])
     scene = conference_standin()
     receiver = receiver_local()
+    t_setup = time.perf_counter()
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
-        if dist.is_initialized():  # one GPU per process: share rank 0's RCCL id, then ncclCommInitRank
-            uid = [RenderGroup.unique_id() if rank == 0 else None]
-            D.broadcast_object(uid)
-            g = RenderGroup.rank(settings, world, rank, uid[0], scene=scene, receiver=receiver)
+        if plan["mode"] == "rank":
+            uid = share_unique_id(rank, world, os.environ, RenderGroup.unique_id)
+            g = RenderGroup.rank(settings, world, rank, uid, scene=scene, receiver=receiver)
         else:
-            g = RenderGroup(settings, devices=[local], scene=scene, receiver=receiver)
+            g = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
+    ranks = Ranks(g, plan["mode"])
+    ranks.barrier()
+    if plan["mode"] == "rank" and rank == 0 and world > 1:
+        with contextlib.suppress(OSError):
+            os.remove(uid_path(os.environ))
+    if g.n_ranks != world:
+        raise SystemExit(f"bench.py: the group has {g.n_ranks} ranks, --gpus asked for {world}")
     g.setEmitterPosInOptix(CONFERENCE_EMITTER)
     g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-    m = g.member(0)
-    # one dedicated (non-null) stream for the renderer, RCCL and the timing events
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    m.set_stream(stream.cuda_stream)
-    ir_len = m.ir_length
+    members = g.members
+    ir_len = members[0].ir_length
     audio_np, sr = reference_audio(wl["audio"])
     assert sr == wl["sample_rate"]
     frames = int(audio_np.size)
-    audio = torch.from_numpy(audio_np).to(dev)
-    out_l = torch.empty_like(audio)
-    out_r = torch.empty_like(audio)
+    bufs = []  # per member: the audio and both output channels, resident on its GPU
+    for m in members:
+        d = m.settings.device
+        bufs.append((DeviceBuffer.from_numpy(d, audio_np), DeviceBuffer(d, 4 * frames), DeviceBuffer(d, 4 * frames)))
 
-    # timing: the renderer's own HIP events around each trace launch and each convolution (on this
-    # stream); no further markers in the timed loop -- each costs the stream a few microseconds
+    # timing: the renderers' own HIP events around each trace launch and each convolution (on
+    # their streams); no further markers in the timed loop -- each costs the stream a few us
     def step():
-        g.render(timed=False)  # clear + trace + RCCL all-reduce + finalize
-        m.convolute_device(audio.data_ptr(), frames, out_l.data_ptr(), out_r.data_ptr())
+        g.render(timed=False)  # clear + trace + RCCL all-reduce + finalize, every GPU
+        for m, (x, ol, orr) in zip(members, bufs):
+            m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    g.synchronize()
     g.stats()
-    D.barrier()
-    torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+    ranks.barrier()
+    g.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
-    D.barrier()
+    g.synchronize()
+    ranks.barrier()
     t1 = time.perf_counter()
-    elapsed = D.max_over_ranks(t1 - t0, dev)
+    elapsed = ranks.max(t1 - t0)
     stats = g.stats()
-    q_rank = int(stats["queries"])  # per step (counters cleared every step)
-    q_all = D.sum_over_ranks(q_rank, dev)
+    q_proc = int(stats["queries"])  # this process's members, per step (counters cleared every step)
+    q_all = int(round(ranks.sum(q_proc)))
+    m0 = members[0]
+    st0 = m0.stats()
+    q_m0 = int(st0["queries"])
     # the trace kernel's own window (direction pre-pass + trace kernel, HIP events on the
-    # renderer's stream) for each of the K timed launches
-    trace_list = m.trace_times(args.steps)
+    # renderer's stream) for each of the K timed launches of GPU 0 of this process
+    trace_list = m0.trace_times(args.steps)
+    assert len(trace_list) == args.steps, (len(trace_list), args.steps)
     trace_ms = float(np.mean(trace_list))
-    conv_list = m.conv_times(args.steps)
-    assert len(conv_list) == args.steps
-    conv_ms = float(np.mean(conv_list))
-    conv_ms_max = D.max_over_ranks(conv_ms, dev)
+    conv_ms_all = []
+    for m in members:
+        cl = m.conv_times(args.steps)
+        assert len(cl) == args.steps, (len(cl), args.steps)
+        conv_ms_all.append(float(np.mean(cl)))
+    conv_ms = conv_ms_all[0]
+    conv_ms_max = ranks.max(max(conv_ms_all))
 
     value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
-    moving = moving_listener(g, D, dev, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
+    moving = moving_listener(g, ranks, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
     bpb = bytes_per_bounce(n_tris)
-    achieved = q_rank * bpb / (trace_ms * 1e-3) / 1e9
-    traffic = load_profile("trace_traffic.json")
-    counts = load_profile(os.path.join("r02", "trace_counts_c3.json"))
-    td = load_profile(os.path.join("r02", "trace_td_c3.json"))
-    vmem = load_profile(os.path.join("r02", "trace_vmem_ceiling.json"))
+    achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
+    traffic, traffic_why = profile_guard(load_profile("trace_traffic.json"), args.workload, st0)
+    counts, counts_why = profile_guard(load_profile(os.path.join("r03", "trace_counts_c3.json")), args.workload, st0,
+                                       ("workload", "tree_hash"))
+    td, td_why = profile_guard(load_profile(os.path.join("r03", "trace_td_c3.json")), args.workload, st0)
+    vmem, vmem_why = profile_guard(load_profile(os.path.join("r03", "trace_vmem_ceiling.json")), args.workload, st0)
     conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02m.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
@@ -374,13 +500,22 @@ def main(argv=None) -> int:
             "sample_rate": wl["sample_rate"],
             "ir_len": ir_len,
             "audio_frames_per_gpu": frames,
-            "parallelism": f"ray-shard x{world}, native RCCL int64 IR all-reduce (arx_group)",
+            "parallelism": (f"ray-shard x{world}, native RCCL int64 IR all-reduce (arx_group: "
+                            + ("one process, ncclCommInitAll over devices " + ",".join(map(str, plan["devices"]))
+                               if plan["mode"] == "local" else f"one process per GPU, ncclCommInitRank, rank {rank}")
+                            + ")"),
         },
+        "runtime": runtime_info(),
+        "setup_s_rank0": setup_s,
         "ray_bounces_per_step": q_all,
         "nominal_ray_bounces_per_s": total_rays * wl["max_bounces"] * args.steps / elapsed,
-        "receiver_hits_per_step_rank0": int(stats["receiver_hits"]),
+        "receiver_hits_per_step_rank0": int(st0["receiver_hits"]),
         "convolved_frames_per_s": conv_frames_s,
         "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms},
+        "trace_kernel_build": {"vgprs": int(st0["trace_vgprs"]), "waves_per_simd": int(st0["trace_waves_per_simd"]),
+                               "waves_target": int(st0["trace_waves_target"]),
+                               "node_format": NODE_FORMATS.get(int(st0["trace_format"]), str(st0["trace_format"])),
+                               "tree_hash": f"{int(st0['tree_hash']):016x}"},
         "roofline": {
             "kernel": "trace_kernel",
             "bound": "hbm",
@@ -388,10 +523,9 @@ def main(argv=None) -> int:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": (traffic or {}).get("bytes_per_launch") if traffic and traffic.get("workload") == args.workload
-            else None,
+            "traffic": traffic.get("bytes_per_launch") if traffic else None,
             "traffic_source": "profiles/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
-                              "and workload; PMC counters cannot be read inside this run)",
+                              "build, tree and workload; PMC counters cannot be read inside this run): " + traffic_why,
             "algorithmic_bytes_per_bounce": bpb,
             "trace_launch_ms": trace_ms,
         },
@@ -408,33 +542,38 @@ def main(argv=None) -> int:
                               "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
-    if vmem and counts and args.workload == "c3":
+    if vmem and counts:
         # the trace's divergent 16-B gathers against their microbenchmark-calibrated ceiling for this
         # kernel's L1 / L2 / Infinity-Cache hit mix (tools/vmem_ceiling.py)
-        lane_rate = counts["lane_loads_16B_per_query"] * q_rank / (trace_ms * 1e-3)
+        lane_rate = counts["lane_loads_16B_per_query"] * q_m0 / (trace_ms * 1e-3)
         result["roofline_vmem"] = {
             "kernel": "trace_kernel", "bound": "vector-memory gathers (L1/L2/Infinity-Cache mix)",
             "achieved": lane_rate, "peak": vmem["ceiling_lane_loads_per_s"], "unit": "16-B lane loads/s",
             "frac": lane_rate / vmem["ceiling_lane_loads_per_s"],
             "mix": {"l1": vmem["fraction_l1"], "l2_hit": vmem["fraction_l2_hit"], "l2_miss": vmem["fraction_l2_miss"]},
-            "source": "profiles/r02/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix)",
+            "source": "profiles/r03/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix): " + vmem_why,
         }
-    if td and args.workload == "c3":
-        # the trace kernel's real ceiling: the texture-data (TD) return path, busy 0.9 of every CU-cycle
+    else:
+        result["roofline_vmem"] = None
+        result["roofline_vmem_why"] = f"vmem ceiling {vmem_why}; lane counts {counts_why}"
+    if td:
+        # the trace kernel's vector-memory return path (TD), busy fraction per CU-cycle
         result["roofline_td"] = {
             "kernel": "trace_kernel", "bound": "td", "achieved": td["td_busy_per_cu_cycle"], "peak": 1.0,
             "unit": "TD busy cycles per CU-cycle", "frac": td["td_busy_per_cu_cycle"],
-            "ta_busy": td["ta_busy_per_cu_cycle"], "source": td["source"],
+            "ta_busy": td["ta_busy_per_cu_cycle"], "source": td["source"] + ": " + td_why,
         }
-    if counts and args.workload == "c3":
-        lanes = counts["lane_loads_16B_per_query"] * q_rank
+    else:
+        result["roofline_td"] = None
+        result["roofline_td_why"] = td_why
+    if counts:
+        lanes = counts["lane_loads_16B_per_query"] * q_m0
         result["vector_memory"] = {
             "node_steps_per_query": counts["steps_per_query"], "tri_tests_per_query": counts["tri_tests_per_query"],
             "lane_loads_16B_per_query": counts["lane_loads_16B_per_query"],
             "lane_loads_per_s": lanes / (trace_ms * 1e-3),
             "l1_side_GBps": 16 * lanes / (trace_ms * 1e-3) / 1e9,
-            "source": "profiles/r02/trace_counts_c3.json (counting build, tools/trace_counts.py); TD busy per CU-cycle "
-                      "from rocprofv3 --pmc in profiles/r02/pmc_*.txt",
+            "source": "profiles/r03/trace_counts_c3.json (counting build, tools/trace_counts.py): " + counts_why,
         }
     if moving is not None:
         result["moving_listener"] = moving
@@ -443,14 +582,16 @@ def main(argv=None) -> int:
             result["moving_listener_rank_of_8"] = moving_listener_rank_shape(settings, scene, receiver,
                                                                              args.c5_frames, shard)
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
-        result["streaming"] = streaming_leg(m, audio_np, 4096, dev)
+        result["streaming"] = streaming_leg(m0, audio_np, 4096)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, receiver, wl, total_rays, audio_np, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    for b in bufs:
+        for x in b:
+            x.close()
+    ranks.barrier()
     g.close()
-    if dist.is_initialized():
-        dist.destroy_process_group()
     return 0
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ARX_ABI_VERSION 1
+#define ARX_ABI_VERSION 2
 
 typedef enum arx_status {
     ARX_OK = 0,
@@ -64,6 +64,16 @@ typedef struct arx_stats {
     double conv_ms;          /* device time of the last convolution */
     int64_t n_scene_tris, n_receiver_tris, n_nodes;
     int32_t bvh_depth;
+    /* guards for stored profiles (bench.py): the scene tree's content hash (nodes + triangle
+     * records of the static scene), and the production trace kernel's register allocation as the
+     * runtime reports it (hipFuncGetAttributes) with the waves per SIMD it admits and the waves per
+     * SIMD the persistent launch is sized for (a mismatch means the compiler changed the
+     * allocation: the launch would leave SIMDs unevenly loaded) */
+    uint64_t tree_hash;
+    int32_t trace_vgprs;
+    int32_t trace_waves_per_simd;
+    int32_t trace_waves_target;
+    int32_t trace_format;    /* node format of the last trace launch: 0 f32, 1 16-bit quantized */
 } arx_stats;
 
 const char* arx_status_string(arx_status s);
@@ -80,6 +90,22 @@ arx_status arx_get_config(const arx_renderer* r, arx_config* out);
  * renderer starts on a non-blocking stream of its own; arx_get_stream returns the current one. */
 arx_status arx_set_stream(arx_renderer* r, void* hip_stream);
 void* arx_get_stream(const arx_renderer* r);
+
+/* ---- Device buffers and runtime -------------------------------------------------------------
+ * Small helpers so that a caller (bench.py, a C host) needs no other GPU framework for its device
+ * buffers and can see which HIP / RCCL runtime libarx resolved.  No reference equivalent (its
+ * CUDABuffer, CUDABuffer.h:10-68, is internal). */
+int32_t arx_device_count(void); /* HIP devices visible to this process; < 0 on error */
+arx_status arx_device_alloc(int32_t device, size_t bytes, void** out);
+void arx_device_free(int32_t device, void* p);
+/* Synchronous copy between any two of host / device memory (hipMemcpyDefault). */
+arx_status arx_memcpy(int32_t device, void* dst, const void* src, size_t bytes);
+/* "hip=<path of the loaded libamdhip64> (runtime version) rccl=<path of the loaded librccl>
+ * (version)" into buf[len]. */
+arx_status arx_runtime_info(char* buf, size_t len);
+/* Scene trees built by this process so far (arx_set_scene / arx_group_set_scene): a group builds
+ * its tree once and shares it between its members. */
+uint64_t arx_scene_build_count(void);
 
 /* Static scene geometry: AudioRenderer::buildAccel + buildSBT (AudioRenderer.cpp:95-218, 413-464),
  * with getMaterialAbsorption (:34-56) already applied per triangle by the caller
@@ -134,13 +160,18 @@ arx_status arx_finalize_ir(arx_renderer* r);
 arx_status arx_ir_device(arx_renderer* r, float** d_left, float** d_right, size_t* ir_len);
 arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir_len);
 arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
-/* Device times (HIP events on the renderer's stream) of the last min(n, 64) trace launches, oldest
+/* Device times (HIP events on the renderer's stream) of the last min(n, arx_timing_ring()) trace launches, oldest
  * first, into ms[0..*n_out); synchronises on them.  The reference's timed window (Time taken by
  * Optix, AudioRenderer.cpp:495-518), kept per launch so a benchmark can average a timed region. */
 arx_status arx_trace_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 /* The same for the last min(n, 64) file convolutions (arx_convolute_device / _audio_file; the
  * reference's "Time taken just to convolute", AudioRenderer.cpp:688-696). */
 arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
+/* The same for the last min(n, 64) live-path convolutions (arx_convolute_live_* and the streaming
+ * convolution's blocks, arx_stream_process*). */
+arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
+/* Capacity of the per-launch timing rings above (launches kept). */
+int32_t arx_timing_ring(void);
 /* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */
@@ -176,8 +207,12 @@ int32_t arx_group_members(const arx_group* g); /* renderers in this process */
 int32_t arx_group_ranks(const arx_group* g);   /* G: shards of the launch */
 /* Member i's renderer (owned by the group; NULL if out of range) for convolution / IR access. */
 arx_renderer* arx_group_member(arx_group* g, int32_t i);
-/* The single-renderer setters, applied to every member. */
+/* The scene tree is built ONCE per group on the host and shared by every member (each uploads it
+ * to its own device); in a one-GPU-per-process group (arx_group_create_rank) this is collective:
+ * rank 0 builds and the tree goes to the other ranks with one RCCL broadcast over xGMI, so every
+ * rank must call it (their arrays are not read). */
 arx_status arx_group_set_scene(arx_group* g, const float* tri_vertices, const float* tri_absorption, int64_t n_tris);
+/* The single-renderer setters, applied to every member. */
 arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_vertices_local, int64_t n_tris);
 arx_status arx_group_set_emitter(arx_group* g, float x, float y, float z);
 arx_status arx_group_set_listener(arx_group* g, float x, float y, float z, float yaw_deg);
@@ -194,6 +229,10 @@ arx_status arx_group_synchronize(arx_group* g);
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
 /* Queries / receiver hits / misses summed over this process's members; times = the longest. */
 arx_status arx_group_get_stats(arx_group* g, arx_stats* out);
+/* values[0..n) of this process combined over all processes of the group (op 0 = sum, 1 = max)
+ * with one RCCL all-reduce, in place; synchronising, so it doubles as a barrier.  A group whose
+ * members all live in this process returns values unchanged. */
+arx_status arx_group_allreduce_f64(arx_group* g, double* values, size_t n, int op);
 
 /* AudioRenderer::convoluteAudioFile (AudioRenderer.h:31; AudioRenderer.cpp:663-750) over
  * convoluteFromAudioBuffer (kernels.cuh:21; kernels.cu:382-438): 1-s blocks zero padded to
@@ -247,6 +286,17 @@ arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);
+/* Host only: build the scene tree, turn it into the byte image a rank-0 build broadcasts to the
+ * other ranks (arx_group_set_scene), read it back and check it is the same tree; returns the tree's
+ * content hash (arx_stats::tree_hash) and the image size. */
+arx_status arx_debug_scene_roundtrip(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
+                                     uint64_t* tree_hash, uint64_t* image_bytes);
+/* The device node arrays as the last trace used them (synchronises): n_nodes coded f32 nodes
+ * (64 B each) into cnodes and their 16-bit quantized copy (32 B each, made on the device) into
+ * qnodes (either may be NULL), the quantization grid (origin xyz, scale xyz) into grid[6], and the
+ * device re-quantizations issued so far into *requants. */
+arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, size_t n_nodes, float* grid,
+                                 uint64_t* requants);
 /* Raw device counters of the last trace (n <= 8): [0] queries [1] receiver hits [2] misses. */
 arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
 /* Force the trace kernel's fallback paths (parity tests of the paths real scenes rarely take):

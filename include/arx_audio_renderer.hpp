@@ -115,17 +115,39 @@ class AudioRenderer {
         }
     }
 
-    void render(double* render_time = nullptr) {  // :27
+    // :27 -- with the write-IR flag set, the IR is dumped once to output_ir_{left,right}.txt
+    // (experimentation/output_ir_*_<stamp>.txt in experimentation mode) and the flag cleared, as
+    // AudioRenderer.cpp:525-567 does
+    void render(double* render_time = nullptr) {
         check(arx_group_render(g_, render_time));
         if (!render_time) check(arx_group_synchronize(g_));
+        if (!write_ir_) return;
+        std::vector<float> l(ir_length_), r(ir_length_);
+        getIR(l.data(), r.data());
+        std::string lp = "output_ir_left.txt", rp = "output_ir_right.txt";
+        if (experimentation_) {
+            const std::string stamp = std::to_string(std::chrono::system_clock::now().time_since_epoch().count());
+            lp = "experimentation/output_ir_left_" + stamp + ".txt";
+            rp = "experimentation/output_ir_right_" + stamp + ".txt";
+        }
+        check(arx_write_float_lines(lp.c_str(), l.data(), l.size()));
+        check(arx_write_float_lines(rp.c_str(), r.data(), r.size()));
+        write_ir_ = false;
     }
 
-    // :31 -- sizes in bytes, host buffers owned by the caller (convolved on the first GPU)
+    // :31 -- sizes in bytes, host buffers owned by the caller (convolved on the first GPU); with
+    // the write-output flag set, the result is dumped once to output_convolute_{left,right}.txt
+    // and the flag cleared (AudioRenderer.cpp:720-744)
     void convoluteAudioFile(float* h_inputBuffer, size_t h_inputBufferSize, float* h_outputBuffer_left,
                             float* h_outputBuffer_right, double* convolute_time = nullptr,
                             double* convolute_process_time = nullptr) {
         check(arx_convolute_audio_file(h_, h_inputBuffer, h_inputBufferSize, h_outputBuffer_left, h_outputBuffer_right,
                                        convolute_time, convolute_process_time));
+        if (!write_output_) return;
+        const size_t n = h_inputBufferSize / sizeof(float);
+        check(arx_write_float_lines("output_convolute_left.txt", h_outputBuffer_left, n));
+        check(arx_write_float_lines("output_convolute_right.txt", h_outputBuffer_right, n));
+        write_output_ = false;
     }
 
     void setEmitterPosInOptix(Vec3 p) { check(arx_group_set_emitter(g_, p.x, p.y, p.z)); }  // :33
@@ -154,33 +176,11 @@ class AudioRenderer {
         if (samplesRecordBuffer) samplesRecordBuffer->add(live_scratch_.data(), live_scratch_.size());
     }
 
-    // text dumps (AudioRenderer.cpp:525-567, 720-744; setters :780-788): the next render writes
-    // output_ir_{left,right}.txt, the next file convolution output_convolute_{left,right}.txt
+    // text dumps (AudioRenderer.cpp:525-567, 720-744; setters :780-788): the next render() writes
+    // output_ir_{left,right}.txt, the next convoluteAudioFile() output_convolute_{left,right}.txt
     void set_write_ir_to_file_flag(bool v) { write_ir_ = v; }
     void set_write_output_to_file_flag(bool v) { write_output_ = v; }
     void enable_experimentation() { experimentation_ = true; }
-    void renderWithDumps(double* render_time = nullptr) {
-        render(render_time);
-        if (!write_ir_) return;
-        std::vector<float> l(ir_length_), r(ir_length_);
-        getIR(l.data(), r.data());
-        std::string lp = "output_ir_left.txt", rp = "output_ir_right.txt";
-        if (experimentation_) {
-            const std::string stamp = std::to_string(std::chrono::system_clock::now().time_since_epoch().count());
-            lp = "experimentation/output_ir_left_" + stamp + ".txt";
-            rp = "experimentation/output_ir_right_" + stamp + ".txt";
-        }
-        check(arx_write_float_lines(lp.c_str(), l.data(), l.size()));
-        check(arx_write_float_lines(rp.c_str(), r.data(), r.size()));
-        write_ir_ = false;
-    }
-    void convoluteAudioFileWithDumps(float* in, size_t bytes, float* outL, float* outR) {
-        convoluteAudioFile(in, bytes, outL, outR);
-        if (!write_output_) return;
-        check(arx_write_float_lines("output_convolute_left.txt", outL, bytes / sizeof(float)));
-        check(arx_write_float_lines("output_convolute_right.txt", outR, bytes / sizeof(float)));
-        write_output_ = false;
-    }
 
     void getIR(float* left, float* right) { check(arx_group_copy_ir(g_, left, right, ir_length_)); }
     arx_stats stats() {

@@ -66,7 +66,7 @@ inline int audio_handler_with_mic(void* outputBuffer, void* inputBuffer, unsigne
 }
 
 // The same duplex callback over the streaming convolution (arx_stream_*, d->stream created with
-// block_frames = the stream's nBufferFrames): the output block is the linear convolution of the
+// block_frames = the stream's nBufferFrames; any other buffer size aborts the stream): the output block is the linear convolution of the
 // mic stream with the IR, one block of latency, no circular wrap and no CircularBuffer.
 inline int audio_handler_with_mic_stream(void* outputBuffer, void* inputBuffer, unsigned int nBufferFrames,
                                          double /*streamTime*/, unsigned int /*status*/, void* data) {
@@ -76,7 +76,9 @@ inline int audio_handler_with_mic_stream(void* outputBuffer, void* inputBuffer, 
     std::unique_lock<std::mutex> lock;
     if (d->renderer_mutex) lock = std::unique_lock<std::mutex>(*d->renderer_mutex, std::try_to_lock);
     int32_t block = 0;
-    if (!d->stream || arx_stream_info(d->stream, &block, nullptr, nullptr) != ARX_OK || nBufferFrames > (unsigned)block)
+    // the stream consumes exactly one block per call: a shorter device buffer would be zero padded
+    // to a full block (gaps in the input timeline) and lose the tail of every output block
+    if (!d->stream || arx_stream_info(d->stream, &block, nullptr, nullptr) != ARX_OK || nBufferFrames != (unsigned)block)
         return 1;
     if ((d->is_rendering && d->is_rendering->load()) || (d->renderer_mutex && !lock.owns_lock())) {
         for (unsigned i = 0; i < 2 * nBufferFrames; ++i) out[i] = 0.0;

@@ -2,15 +2,20 @@
 // on the GPU: the reference's export_audio flow (R/prebuild/obj_raytracer/main.cpp:653-718) plus one
 // mic callback (audioHandlerWithMic, main.cpp:99-135), through libarx.so's group API.
 //
-//   export_demo config.json leftHalf.obj rightHalf.obj out_dir devices(e.g. "0" or "0,0,0,0")
+//   export_demo config.json leftHalf.obj rightHalf.obj out_dir devices(e.g. "0" or "0,0,0,0") [dumps]
 //
 // Loads config.json (Context::loadContext), the OBJ scene and the receiver halves (loadOBJ,
 // HalfSphere), the WAV (AudioFile), renders, convolves the file (convoluteAudioFile), runs one
 // 4096-frame live block into a CircularBuffer (convoluteLiveInput), and writes raw results to
 // out_dir for tests/test_gpu_shim.py to compare with the CPU oracle:
 //   ir_left.f32 ir_right.f32 conv_left.f32 conv_right.f32 live.f64, and a stats line on stdout.
+// With "dumps", it then replays key P of main.cpp:317-322 inside out_dir: render, set both write
+// flags, render again (writes output_ir_{left,right}.txt, AudioRenderer.cpp:525-567), convolve
+// (writes output_convolute_{left,right}.txt, :720-744); a further render + convolve must write
+// nothing (the flags reset after one write).
 #include <cstdio>
 #include <cstdlib>
+#include <unistd.h>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -76,6 +81,29 @@ int main(int argc, char** argv) {
         r.convoluteLiveInput(mic.data(), mic.size() * sizeof(double), &cb);
         const std::vector<double> live = cb.get_and_reset(2 * mic.size());
         write_raw(out + "/live.f64", live.data(), live.size() * 8);
+        if (argc > 6 && std::string(argv[6]) == "dumps") {
+            if (chdir(out.c_str()) != 0) return 2;
+            r.render();
+            r.set_write_ir_to_file_flag(true);
+            r.set_write_output_to_file_flag(true);
+            r.render();
+            r.convoluteAudioFile(x.data(), x.size() * sizeof(float), cl.data(), cr.data());
+            const char* dumps[4] = {"output_ir_left.txt", "output_ir_right.txt", "output_convolute_left.txt",
+                                    "output_convolute_right.txt"};
+            for (const char* f : dumps)
+                if (std::rename(f, (std::string(f) + ".first").c_str()) != 0) {
+                    std::fprintf(stderr, "%s was not written\n", f);
+                    return 3;
+                }
+            r.render();
+            r.convoluteAudioFile(x.data(), x.size() * sizeof(float), cl.data(), cr.data());
+            for (const char* f : dumps)
+                if (access(f, F_OK) == 0) {
+                    std::fprintf(stderr, "%s written twice (the flag did not reset)\n", f);
+                    return 4;
+                }
+            std::printf("dumps ok\n");
+        }
         const arx_stats st = r.stats();
         std::printf("queries %llu receiver_hits %llu misses %llu gpus %d render_ms %.3f conv_ms %.3f\n",
                     (unsigned long long)st.queries, (unsigned long long)st.receiver_hits, (unsigned long long)st.misses,

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # and the ctypes binding covers all of them
     assert set(declared) <= set(_lib.SIGNATURES), set(declared) - set(_lib.SIGNATURES)
-    assert L.arx_abi_version() == 1
+    assert L.arx_abi_version() == 2
 
 
 def test_status_strings_and_errors():
@@ -94,3 +94,30 @@ def test_no_silent_fallback_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.ArxError):
         _lib.lib()
+
+
+def test_scene_image_roundtrip_and_hash(c1_scene):
+    """The byte image rank 0 broadcasts to the other ranks (arx_group_set_scene) reads back as the
+    same tree; the content hash (arx_stats.tree_hash, the stored-profile guard) is stable across
+    builds and changes with the geometry."""
+    L = _lib.lib()
+    tv = np.ascontiguousarray(c1_scene.tri_v, np.float32)
+    ta = np.ascontiguousarray(c1_scene.tri_abs, np.float32)
+
+    def roundtrip(v, a):
+        h, n = C.c_uint64(), C.c_uint64()
+        _lib.check(L.arx_debug_scene_roundtrip(_lib.fptr(v), _lib.fptr(a), a.size, C.byref(h), C.byref(n)))
+        return h.value, n.value
+
+    before = L.arx_scene_build_count()
+    h1, n1 = roundtrip(tv, ta)
+    h2, n2 = roundtrip(tv, ta)
+    assert L.arx_scene_build_count() == before + 2
+    assert h1 == h2 and n1 == n2 and n1 > 64 * len(ta) // 4
+    tv2 = tv.copy()
+    tv2[0, 0] += 0.25
+    assert roundtrip(tv2, ta)[0] != h1
+    bad = ta.copy()
+    bad[0] = 1.5  # absorption outside [0, 1]
+    h, n = C.c_uint64(), C.c_uint64()
+    assert L.arx_debug_scene_roundtrip(_lib.fptr(tv), _lib.fptr(bad), bad.size, C.byref(h), C.byref(n)) == 1

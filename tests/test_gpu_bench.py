@@ -40,3 +40,30 @@ def test_bench_prints_one_contract_line():
         assert k in cb, k
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
     assert d["moving_listener"]["frames"] == 3
+    # libarx ran on the ROCm runtime it was built against (no other GPU framework in the process)
+    assert "/opt/rocm" in d["runtime"].split("rccl=")[1], d["runtime"]
+    assert d["trace_kernel_build"]["waves_per_simd"] == d["trace_kernel_build"]["waves_target"]
+
+
+def test_bench_refuses_more_gpus_than_the_box_has():
+    from audiorenderingv2_amd import device_count
+
+    n = device_count() + 1
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "1"], cwd=REPO,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert f"--gpus {n}" in p.stderr
+
+
+def test_bench_rank_path_under_torchrun():
+    """The one-GPU-per-process path (torch.distributed.run, ncclCommInitRank, RCCL barriers and
+    max-over-ranks timing) rehearsed at one rank."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", "29631", os.path.join(REPO, "bench.py"), "--gpus", "1", "--process-group",
+           "--workload", "c2", "--steps", "2", "--warmup", "1", "--c5-frames", "3", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and "ncclCommInitRank" in d["config"]["parallelism"] and d["value"] > 0

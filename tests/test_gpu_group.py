@@ -93,6 +93,30 @@ def test_oversubscribed_group_shards_exact(conference, n):
     assert same(g.get_ir(), f.get_ir())
 
 
+def test_oversubscribed_group_back_to_back_renders(conference):
+    """Two renders with different seeds issued without a host synchronisation in between: the
+    second render's clears must not overtake the first one's histogram copies (every member
+    must end with exactly the second launch's IR)."""
+    s = RenderSettings(rays=(50, 40, 10), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.25)
+    refs = {}
+    for seed in (11, 12):
+        r = single(conference, RenderSettings(**{**s.__dict__, "seed": seed}))
+        r.render()
+        refs[seed] = r.get_ir()
+        r.close()
+    assert not same(refs[11], refs[12])
+    g = make_group(conference, s, [0] * 4)
+    for _ in range(3):
+        g.set_seed(11)
+        g.render(timed=False)
+        g.set_seed(12)
+        g.render(timed=False)
+        g.synchronize()
+        for m in g.members:
+            assert same(m.get_ir(), refs[12])
+    g.close()
+
+
 def test_group_rejects_mixed_device_lists():
     from audiorenderingv2_amd import ArxError
 

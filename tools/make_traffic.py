@@ -7,7 +7,10 @@ TCC_EA0_RDREQ x 64 B while the requests are 128 B, so it is doubled; WRITE_SIZE 
 the histogram's one-dword atomics.  Infinity-Cache hits are included (the guide: they are
 counted, not excluded), so this is an upper bound on HBM traffic.
 
-    python tools/make_traffic.py gpurun_out/pmc_traffic [workload] [out.json]
+    python tools/make_traffic.py gpurun_out/pmc_traffic [workload] [out.json] [guard.json]
+
+guard.json (tools/trace_once.py ARX_GUARD_OUT) carries the profiled run's tree hash and trace kernel
+VGPRs; bench.py reports the traffic only for a run that matches them.
 """
 import csv
 import glob
@@ -47,6 +50,10 @@ def main() -> int:
         "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH_SIZE x2 (gfx950 128-B "
                   "requests tallied at 64 B), Infinity-Cache hits included: upper bound on HBM bytes",
     }
+    if len(sys.argv) > 4:
+        with open(sys.argv[4]) as fh:
+            guard = json.load(fh)
+        out.update({k: guard[k] for k in ("tree_hash", "trace_vgprs") if k in guard})
     path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "trace_traffic.json")
     with open(path, "w") as fh:

@@ -2,7 +2,10 @@
 """Render the C3 bench workload a few times (for profilers and A/B runs).
 
     python tools/trace_once.py [n_renders]      # library: ARX_LIB (default: the product libarx.so)
-Prints the median trace-kernel time (HIP events) over the renders after the first."""
+Prints the median trace-kernel time (HIP events) over the renders after the first; with
+ARX_GUARD_OUT=path it also writes the run's profile guard (workload, tree hash, trace kernel VGPRs:
+bench.py only uses a stored profile whose guard matches its own run)."""
+import json
 import os
 import sys
 
@@ -28,6 +31,11 @@ st = r.stats()
 irl, irr = r.get_ir()
 chk = int(np.frombuffer(irl.tobytes() + irr.tobytes(), np.uint32).astype(np.uint64).sum())
 med = float(np.median(ms[1:] if n > 1 else ms))
+if os.environ.get("ARX_GUARD_OUT"):
+    with open(os.environ["ARX_GUARD_OUT"], "w") as fh:
+        json.dump({"workload": "c3" if rays == (100, 100, 100) and s.max_bounces == 16 else f"rays{rays}",
+                   "tree_hash": f"{int(st['tree_hash']):016x}", "trace_vgprs": int(st["trace_vgprs"]),
+                   "trace_format": int(st["trace_format"])}, fh)
 print(f"trace {med:.3f} ms (median of {max(n - 1, 1)}) queries {st['queries']} nodes {st['n_nodes']} "
       f"depth {st['bvh_depth']} ir_checksum {chk} lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}",
       flush=True)
