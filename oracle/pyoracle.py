@@ -172,6 +172,20 @@ class Scene:
                         R.ctypes.data_as(I64), C.byref(st), threads)
         return L, R, {"queries": st.queries, "receiver_hits": st.receiver_hits, "misses": st.misses}
 
+    def float_sums(self, p: OrcParams, ray_begin: int, ray_end: int):
+        """orc_trace_float_sums: (int64 L, R), (f64 L, R), (f32 L, R), stats of the same rays."""
+        n = p.ir_length
+        L, R = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        dL, dR = np.zeros(n, np.float64), np.zeros(n, np.float64)
+        fL, fR = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        st = OrcStats()
+        I64, D, F = C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_float)
+        lib().orc_trace_float_sums(C.byref(self.s), C.byref(p), ray_begin, ray_end, L.ctypes.data_as(I64),
+                                   R.ctypes.data_as(I64), dL.ctypes.data_as(D), dR.ctypes.data_as(D),
+                                   fL.ctypes.data_as(F), fR.ctypes.data_as(F), C.byref(st))
+        return (L, R), (dL, dR), (fL, fR), {"queries": st.queries, "receiver_hits": st.receiver_hits,
+                                             "misses": st.misses}
+
     def records(self, p: OrcParams, first: int, count: int) -> np.ndarray:
         rec = (OrcRayRecord * count)()
         lib().orc_trace_records(C.byref(self.s), C.byref(p), first, count, rec)
