@@ -23,6 +23,10 @@
 
 using namespace arx;
 
+#ifndef ARX_TRACE_PROF
+#define ARX_TRACE_PROF 0  // measurement builds only (build.py --exp TAG -D ARX_TRACE_PROF=1)
+#endif
+
 namespace {
 thread_local std::string g_last_error;
 }  // namespace
@@ -170,6 +174,30 @@ arx_status prepare_receiver_model(arx_renderer* r) {
     std::vector<int32_t> lv(order);
     lv.insert(lv.end(), start.begin(), start.end());
     ARX_HIP(hipMemcpyAsync(r->d_recv_levels, lv.data(), lv.size() * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
+    // the receiver's CW4 layout (root at unit kW4RecvRoot, blocks after the scene's) for the refit
+    collapse_w4(r->recv, base, (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot, r->scene_img->w4.unit_end, r->recv4);
+    std::vector<int32_t> w4n(11 * r->recv4.nodes.size()), w4t(2 * r->recv4.leaf_tris.size());
+    for (size_t i = 0; i < r->recv4.nodes.size(); ++i) {
+        std::copy(r->recv4.src.begin() + 8 * i, r->recv4.src.begin() + 8 * i + 8, w4n.begin() + 11 * i);
+        w4n[11 * i + 8] = (int32_t)r->recv4.nodes[i].meta;
+        w4n[11 * i + 9] = (int32_t)r->recv4.nodes[i].base;
+        w4n[11 * i + 10] = (int32_t)r->recv4.nodes[i].self;
+    }
+    for (size_t i = 0; i < r->recv4.leaf_tris.size(); ++i) {
+        w4t[2 * i] = (int32_t)r->recv4.leaf_tris[i].first;
+        w4t[2 * i + 1] = r->recv4.leaf_tris[i].second;
+    }
+    hipFree(r->d_recv_w4);
+    hipFree(r->d_recv_w4_tris);
+    r->d_recv_w4 = nullptr;
+    r->d_recv_w4_tris = nullptr;
+    ARX_HIP(hipMalloc(&r->d_recv_w4, std::max<size_t>(1, w4n.size()) * sizeof(int32_t)));
+    ARX_HIP(hipMalloc(&r->d_recv_w4_tris, std::max<size_t>(1, w4t.size()) * sizeof(int32_t)));
+    if (!w4n.empty())
+        ARX_HIP(hipMemcpyAsync(r->d_recv_w4, w4n.data(), w4n.size() * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
+    if (!w4t.empty())
+        ARX_HIP(hipMemcpyAsync(r->d_recv_w4_tris, w4t.data(), w4t.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                               r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));  // pageable sources
     r->recv_level_count = (int32_t)order.size();
     return ARX_OK;
@@ -225,6 +253,8 @@ arx_status ensure_device_scene(arx_renderer* r) {
         }
         build_bvh(tv.data(), ab.data(), 0.0f, (int64_t)ab.size(), (int32_t)img.n_input, r->recv);
         relocate_bvh(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size());
+        collapse_w4(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot,
+                    img.w4.unit_end, r->recv4);
     }
     const size_t n_nodes = 1 + sc.nodes.size() + r->recv.nodes.size();
     const size_t n_tris = sc.tris.size() + r->recv.tris.size();
@@ -248,6 +278,28 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
+    // CW4: the buffer holds the scene's units, then the receiver's; the f32 records are the top node,
+    // the scene's nodes and (host-built receivers) the receiver's
+    const size_t w_units = std::max<size_t>(r->recv4.unit_end, img.w4.unit_end);
+    const size_t host_recv_w4 = r->recv_refit ? 0 : r->recv4.nodes.size();
+    const size_t n_w4f = 1 + img.w4.nodes.size() + host_recv_w4;
+    if (w_units > r->wbuf_cap) {
+        if (r->d_wbuf) ARX_HIP(hipFree(r->d_wbuf));
+        r->d_wbuf = nullptr;
+        const size_t cap = w_units + 4096;
+        ARX_HIP(hipMalloc(&r->d_wbuf, cap * 16));
+        r->wbuf_cap = cap;
+        full = true;
+    }
+    if (n_w4f > r->w4f_cap) {
+        if (r->d_w4f) ARX_HIP(hipFree(r->d_w4f));
+        r->d_w4f = nullptr;
+        const size_t cap = n_w4f + 1024;
+        ARX_HIP(hipMalloc(&r->d_w4f, cap * sizeof(W4NodeF)));
+        r->w4f_cap = cap;
+        full = true;
+    }
+    r->n_w4f = n_w4f;
     // The quantization grid: made when the scene changes, grown when the receiver leaves it (a
     // listener walking out of the room): the new grid spans the old one, the scene, the receiver
     // and the emitter with half the extent as margin, so such a walk re-grids once or twice, not
@@ -308,6 +360,47 @@ arx_status ensure_device_scene(arx_renderer* r) {
         if (host_recv && !r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + sc.tris.size(), r->recv.tris.data(), r->recv.tris.size() * sizeof(TriRec),
                                    hipMemcpyHostToDevice, r->stream));
+        // CW4: the scene's buffer image and node records once per scene; the top node's record
+        // (child 0 the scene root, child 1 the host-built receiver's root or, on the refit path, a
+        // placeholder the refit kernel replaces); a host-built receiver's records and triangles
+        W4NodeF wtop;
+        std::memset(&wtop, 0, sizeof(wtop));
+        wtop.base = kW4SceneRoot;
+        wtop.self = 0;
+        if (sc.root.count >= 0) {
+            wtop.meta |= 1u;
+            for (int k = 0; k < 3; ++k) {
+                wtop.lo[0][k] = sc.root.lo[k];
+                wtop.hi[0][k] = sc.root.hi[k];
+            }
+        }
+        if (host_recv && r->recv.root.count >= 0) {
+            wtop.meta |= 1u << 2;
+            for (int k = 0; k < 3; ++k) {
+                wtop.lo[1][k] = r->recv.root.lo[k];
+                wtop.hi[1][k] = r->recv.root.hi[k];
+            }
+        }
+        ARX_HIP(hipMemcpyAsync(r->d_w4f, &wtop, sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
+        if (full && !img.wimage.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_wbuf, img.wimage.data(), img.wimage.size() * sizeof(uint32_t),
+                                   hipMemcpyHostToDevice, r->stream));
+        if (full && !img.w4.nodes.empty())
+            ARX_HIP(hipMemcpyAsync(r->d_w4f + 1, img.w4.nodes.data(), img.w4.nodes.size() * sizeof(W4NodeF),
+                                   hipMemcpyHostToDevice, r->stream));
+        std::vector<uint32_t> rimage;
+        if (host_recv) {
+            if (!r->recv4.nodes.empty())
+                ARX_HIP(hipMemcpyAsync(r->d_w4f + 1 + img.w4.nodes.size(), r->recv4.nodes.data(),
+                                       r->recv4.nodes.size() * sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
+            const size_t u0 = img.w4.unit_end;
+            rimage.assign((r->recv4.unit_end - u0) * 4, 0u);
+            for (const auto& lt : r->recv4.leaf_tris)
+                std::memcpy(rimage.data() + (size_t)(lt.first - u0) * 4, &r->recv.tris[(size_t)lt.second], sizeof(TriRec));
+            if (!rimage.empty())
+                ARX_HIP(hipMemcpyAsync(r->d_wbuf + u0, rimage.data(), rimage.size() * sizeof(uint32_t),
+                                       hipMemcpyHostToDevice, r->stream));
+        }
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
     if (regrid || top_changed) {
@@ -317,6 +410,8 @@ arx_status ensure_device_scene(arx_renderer* r) {
         const size_t nq = host_recv ? n_nodes : 1 + sc.nodes.size();
         ARX_HIP(launch_requant16(r->d_cnodes, nq, r->qgrid, r->d_qnodes,
                                  reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
+        ARX_HIP(launch_requant_w4(r->d_w4f, r->n_w4f, r->qgrid, r->d_wbuf,
+                                  reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
         ++r->requants;
     }
     r->q_valid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
@@ -343,6 +438,18 @@ arx_status ensure_device_scene(arx_renderer* r) {
         a.cnodes = r->d_cnodes;
         a.qnodes = r->q_valid ? r->d_qnodes : nullptr;
         a.flag = reinterpret_cast<unsigned int*>(r->d_counters + 6);
+        if (r->q_valid) {  // the CW4 copy follows the quantized one (same grid)
+            a.wbuf = r->d_wbuf;
+            a.w4_nodes = r->d_recv_w4;
+            a.n_w4 = (int32_t)r->recv4.nodes.size();
+            a.w4_tris = r->d_recv_w4_tris;
+            a.n_w4_tris = (int32_t)r->recv4.leaf_tris.size();
+            a.scene_nonempty = sc.root.count >= 0 ? 1 : 0;
+            for (int k = 0; k < 3; ++k) {
+                a.scene_lo[k] = sc.root.lo[k];
+                a.scene_hi[k] = sc.root.hi[k];
+            }
+        }
         if (a.n_tris > 0) ARX_HIP(launch_receiver_refit(a, r->stream));
     }
     r->scene_dirty = false;
@@ -353,6 +460,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
     r->stats.n_nodes = (int64_t)n_nodes;
     r->stats.bvh_depth = 1 + std::max(sc.depth, r->recv.depth);
     r->stats.tree_hash = img.hash;
+    r->depth4 = 1 + std::max(img.w4.depth, r->recv4.depth);
     return ARX_OK;
 }
 
@@ -444,13 +552,25 @@ arx_status arx::check_scene_input(const float* tri_v, const float* tri_abs, int6
     return ARX_OK;
 }
 
+namespace {
+// The parts of a scene image derived from its BVH2: the coded copy, the CW4 collapse and the CW4
+// buffer's triangle image.
+void finish_scene_image(SceneImage& img) {
+    img.coded.resize(img.bvh.nodes.size());
+    code_nodes(img.bvh.nodes.data(), img.bvh.nodes.size(), img.coded.data());
+    collapse_w4(img.bvh, 1, 0, img.bvh.root, kW4SceneRoot, kW4SceneUnit, img.w4);
+    img.wimage.assign((size_t)img.w4.unit_end * 4, 0u);
+    for (const auto& lt : img.w4.leaf_tris)
+        std::memcpy(img.wimage.data() + (size_t)lt.first * 4, &img.bvh.tris[(size_t)lt.second], sizeof(TriRec));
+}
+}  // namespace
+
 SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_t n) {
     auto img = std::make_shared<SceneImage>();
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, img->bvh);
     bfs_prefix_order(img->bvh, 1023);  // the top levels of the scene tree breadth-first (node locality)
     relocate_bvh(img->bvh, 1, 0);
-    img->coded.resize(img->bvh.nodes.size());
-    code_nodes(img->bvh.nodes.data(), img->bvh.nodes.size(), img->coded.data());
+    finish_scene_image(*img);
     img->n_input = n;
     img->hash = scene_hash(img->bvh);
     g_scene_builds.fetch_add(1);
@@ -504,8 +624,7 @@ SceneRef arx::deserialize_scene(const uint8_t* p, size_t n, const char** why) {
     if (!validate_bvh_range(img->bvh.nodes.data(), 1, img->bvh.nodes.size(), 1 + img->bvh.nodes.size(),
                             img->bvh.tris.size(), why))
         return nullptr;
-    img->coded.resize(h.n_nodes);
-    code_nodes(img->bvh.nodes.data(), img->bvh.nodes.size(), img->coded.data());
+    finish_scene_image(*img);
     return img;
 }
 
@@ -615,6 +734,8 @@ arx_status arx_debug_scene_roundtrip(const float* tri_v, const float* tri_abs, i
                       std::memcmp(a->bvh.nodes.data(), b->bvh.nodes.data(), a->bvh.nodes.size() * sizeof(BvhNode)) == 0 &&
                       std::memcmp(a->bvh.tris.data(), b->bvh.tris.data(), a->bvh.tris.size() * sizeof(TriRec)) == 0 &&
                       std::memcmp(a->coded.data(), b->coded.data(), a->coded.size() * sizeof(BvhNode)) == 0 &&
+                      a->wimage == b->wimage && a->w4.nodes.size() == b->w4.nodes.size() &&
+                      std::memcmp(a->w4.nodes.data(), b->w4.nodes.data(), a->w4.nodes.size() * sizeof(W4NodeF)) == 0 &&
                       std::memcmp(&a->bvh.root, &b->bvh.root, sizeof(ChildRef)) == 0;
     if (!same) return fail(ARX_ERR_INTERNAL, "scene image round trip changed the tree");
     if (hash) *hash = a->hash;
@@ -711,10 +832,14 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
             (e = hipEventCreateWithFlags(&r->lev0[i], kTimingEvent)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&r->lev1[i], kTimingEvent)) != hipSuccess)
             return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
-    // the production trace kernel's register allocation, as the runtime sees it (arx_stats)
-    if ((e = trace_kernel_occupancy(true, &r->stats.trace_vgprs, &r->stats.trace_waves_per_simd,
-                                    &r->stats.trace_waves_target)) != hipSuccess)
-        return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
+    // the production trace kernels' register allocation, as the runtime sees it (arx_stats)
+    for (int f = 0; f < 3; ++f)
+        if ((e = trace_kernel_occupancy(f, &r->occ[f][0], &r->occ[f][1], &r->occ[f][2])) != hipSuccess)
+            return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
+    r->stats.trace_vgprs = r->occ[kFmtW4][0];
+    r->stats.trace_waves_per_simd = r->occ[kFmtW4][1];
+    r->stats.trace_waves_target = r->occ[kFmtW4][2];
+    r->stats.trace_format = kFmtW4;
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
@@ -739,9 +864,14 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_tris);
     hipFree(r->d_gstack);
     hipFree(r->d_dirs);
+    hipFree(r->d_prof);
     hipFree(r->d_recv_local);
     hipFree(r->d_recv_nodes);
     hipFree(r->d_recv_levels);
+    hipFree(r->d_recv_w4);
+    hipFree(r->d_recv_w4_tris);
+    hipFree(r->d_wbuf);
+    hipFree(r->d_w4f);
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
@@ -876,6 +1006,8 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     // grid: the slab arithmetic's error bound assumes origins within the grid's extent
     const float* em = r->emitter;
     a.qnodes = (r->q_valid && !r->force_f32_nodes && qgrid_contains(r->qgrid, em, em)) ? r->d_qnodes : nullptr;
+    // the CW4 tree (the default) on the same condition, unless a BVH2 path is forced
+    a.wbuf = (a.qnodes && !r->force_bvh2 && !r->force_global_stack) ? r->d_wbuf : nullptr;
     a.qgrid = r->qgrid;
     a.tris = r->d_tris;
     a.hist = r->hist();
@@ -910,9 +1042,11 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     }
     a.dirs = r->d_dirs;
     const bool gstack = r->force_global_stack || a.bvh_depth + 1 > kLdsStack;
-    if (gstack) {  // trees deeper than the LDS stack: one global column of bvh_depth + 1 entries per lane
+    // CW4: up to three pushes per level; the rows beyond the LDS rows overflow into a global column
+    const size_t w4_rows = (size_t)std::max(1, 3 * r->depth4 + 3 - kLdsStack);
+    if (gstack || a.wbuf) {  // trees deeper than the LDS stack: one global column of bvh_depth + 1 entries per lane
         const size_t lanes = trace_max_lanes(r->cus);
-        const size_t need = (size_t)(a.bvh_depth + 1) * lanes;
+        const size_t need = (a.wbuf ? w4_rows : (size_t)(a.bvh_depth + 1)) * lanes;
         if (need > r->gstack_cap) {
             if (r->d_gstack) ARX_HIP(hipFree(r->d_gstack));
             r->d_gstack = nullptr;
@@ -923,8 +1057,23 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         a.gstack = r->d_gstack;
         a.gstack_lanes = lanes;
     }
+#if ARX_TRACE_PROF  // measurement builds only: per-wave records (arx_debug_trace_profile)
+    {
+        const size_t words = (size_t)r->cus * 64 * kProfWords;  // >= waves of any trace grid
+        if (!r->d_prof) {
+            ARX_HIP(hipMalloc(&r->d_prof, words * sizeof(unsigned long long)));
+            r->prof_words = words;
+        }
+        ARX_HIP(hipMemsetAsync(r->d_prof, 0, words * sizeof(unsigned long long), r->stream));
+        a.prof = r->d_prof;
+    }
+#endif
     const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
-    r->stats.trace_format = a.qnodes ? 1 : 0;
+    const int fmt = a.wbuf ? kFmtW4 : (a.qnodes ? kFmtQ16 : kFmtF32);
+    r->stats.trace_format = fmt;
+    r->stats.trace_vgprs = r->occ[fmt][0];
+    r->stats.trace_waves_per_simd = r->occ[fmt][1];
+    r->stats.trace_waves_target = r->occ[fmt][2];
     ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
@@ -1213,10 +1362,22 @@ arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, si
     return ARX_OK;
 }
 
+arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_words, size_t* n_out) {
+    if (!r || (n_words > 0 && !out)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!r->d_prof) return fail(ARX_ERR_NOT_READY, "not a profiling build (ARX_TRACE_PROF) or no trace yet");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    ARX_HIP(hipStreamSynchronize(r->stream));
+    const size_t k = std::min(n_words, r->prof_words);
+    ARX_HIP(hipMemcpy(out, r->d_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (n_out) *n_out = k;
+    return ARX_OK;
+}
+
 arx_status arx_debug_set_trace_path(arx_renderer* r, int path) {
-    if (!r || path < 0 || path > 3) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!r || path < 0 || path > 7) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
     r->force_f32_nodes = (path & 1) != 0;
     r->force_global_stack = (path & 2) != 0;
+    r->force_bvh2 = (path & 4) != 0;
     return ARX_OK;
 }
 

@@ -12,6 +12,7 @@
 #include "arx_bvh.hpp"
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
+#include "arx_wide.hpp"
 
 namespace arx {
 
@@ -45,9 +46,14 @@ inline uint64_t n_rays(const arx_config& c) {
 struct SceneImage {
     BvhBuild bvh;
     std::vector<BvhNode> coded;
+    W4Build w4;                  // the CW4 copy: scene root at unit 2, blocks from unit kW4SceneUnit
+    std::vector<uint32_t> wimage;  // CW4 buffer units [0, w4.unit_end) x 4 words: leaf triangles
+                                   // filled, node slots zero (quantized on the device)
     int64_t n_input = 0;  // triangles given to arx_set_scene (global ids 0 .. n_input-1)
     uint64_t hash = 0;    // content hash of nodes and triangle records (profile guards)
 };
+// CW4 buffer: top node at unit 0, its block (scene root node, receiver root node) at units 2..5
+constexpr uint32_t kW4SceneRoot = 2, kW4RecvRoot = 4, kW4SceneUnit = 6;
 using SceneRef = std::shared_ptr<const SceneImage>;
 
 // Input checks of arx_set_scene (finite vertices, absorption in [0, 1] or the receiver marks).
@@ -111,6 +117,19 @@ struct arx_renderer {
     // device
     arx::BvhNode* d_cnodes = nullptr;  // coded copy of the tree (code_nodes): the f32 fallback
     arx::QNode2* d_qnodes = nullptr;   // 16-bit quantized copy of d_cnodes (same indices): the default
+    // CW4 copy: buffer, f32 node records (top node, scene, host-built receiver) for the device
+    // re-quantization, the receiver's CW4 layout (refit path) and its device tables
+    uint4* d_wbuf = nullptr;
+    size_t wbuf_cap = 0;           // units
+    arx::W4NodeF* d_w4f = nullptr;
+    size_t w4f_cap = 0;
+    size_t n_w4f = 0;              // records in use
+    arx::W4Build recv4;
+    int32_t* d_recv_w4 = nullptr;  // 11 ints per receiver CW4 node
+    int32_t* d_recv_w4_tris = nullptr;
+    bool force_bvh2 = false;       // arx_debug_set_trace_path bit 2
+    int32_t depth4 = 0;            // CW4 levels (top node included): bounds the stack (3 per level)
+    int32_t occ[3][3] = {};        // per node format: VGPRs, waves admitted, waves targeted
     arx::QGrid qgrid{};
     bool qgrid_set = false;
     bool q_valid = false;         // d_qnodes matches the tree (re-quantized on the device, arx_receiver.hip)
@@ -145,6 +164,8 @@ struct arx_renderer {
 
     std::vector<arx_stream*> streams;  // live streaming convolutions of this renderer (arx_stream_create)
 
+    unsigned long long* d_prof = nullptr;  // per-wave records (profiling builds, ARX_TRACE_PROF)
+    size_t prof_words = 0;
     int32_t last_format = 0;  // node format of the last trace launch (arx_stats::trace_format)
     arx_stats stats;
 };

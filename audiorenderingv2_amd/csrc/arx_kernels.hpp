@@ -25,7 +25,7 @@ hipError_t launch_clear(unsigned long long* hist, uint64_t n, unsigned long long
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
 // Register allocation of the production trace kernel instance (hipFuncGetAttributes numRegs), the
 // waves per SIMD it admits, and the waves per SIMD the persistent grid is sized for.
-hipError_t trace_kernel_occupancy(bool q16, int* vgprs, int* waves_admitted, int* waves_target);
+hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target);
 
 // ---- moving listener (arx_receiver.hip): transform + fixed-topology refit of the receiver ----
 struct RefitArgs {
@@ -47,6 +47,17 @@ struct RefitArgs {
     BvhNode* cnodes;
     QNode2* qnodes;             // null: the quantized copy is not maintained (receiver off the grid)
     unsigned int* flag;         // set if a box fell off the grid (never, given the host's bound)
+    // CW4 copy (null wbuf: not maintained): the receiver's CW4 nodes (11 ints each: the BVH2
+    // (ref, count) of the 4 slots, meta, base, self unit), its leaf triangles ((unit, local index)
+    // pairs) and the top node (unit 0: child 0 = the scene root, unit 2; child 1 = the receiver
+    // root, unit 4)
+    uint4* wbuf;
+    const int32_t* w4_nodes;
+    int32_t n_w4;
+    const int32_t* w4_tris;
+    int32_t n_w4_tris;
+    float scene_lo[3], scene_hi[3];
+    int32_t scene_nonempty;
 };
 size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels);  // bytes of LDS
 hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
@@ -55,6 +66,10 @@ hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
 // no host work or upload.  flag is set if a box falls off the grid.
 hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
                             hipStream_t s);
+// The CW4 nodes of n f32 node records (W4NodeF: top node, scene, host-built receiver) quantized for
+// grid g into the CW4 buffer at their own units (quantize_w4, arx_wide.hpp).
+hipError_t launch_requant_w4(const W4NodeF* nodes, uint64_t n, const QGrid& g, uint4* wbuf, unsigned int* flag,
+                             hipStream_t s);
 
 // ---- convolution (arx_conv.hip) ----
 struct ConvPlan;  // opaque, defined in arx_conv.hip

@@ -52,6 +52,41 @@ struct alignas(16) QNode2 {
 };
 static_assert(sizeof(QNode2) == 32, "QNode2 must be 32 B");
 
+// ---- 4-wide compressed tree (CW4) ------------------------------------------------------------
+// The BVH2 collapsed to 4 children per node (arx_wide.cpp).  Nodes and leaf triangles live in one
+// buffer of 16-B units (wbuf): node N's children form one block at N.base -- its inner children's
+// nodes (2 units each) first, then its leaves' triangle records (3 units each, TriRec), so one
+// 32-bit base addresses both.  A node is 32 B = two 16-B loads (QNode2 needs two as well, for two
+// children instead of four):
+//   w0 = ox | oy << 14 | ex << 28          frame origin (units of 4 grid quanta) and exponents:
+//   w1 = oz | ey << 14 | ez << 18 | meta << 22   axis k spans 4*o_k + [0, 63 * 2^e_k] grid quanta
+//   w2..w6: 24 six-bit planes, five per word at bits 0, 6, 12, 18, 24; child c's planes are
+//           slots 6c .. 6c+5 = x lo, x hi, y lo, y hi, z lo, z hi (plane = 4*o + q * 2^e)
+//   w7 = base (16-B units)
+// meta: 2 bits per child slot: 0 empty, 1 inner, 2 leaf of 1 triangle, 3 leaf of 2; inner slots
+// come first, then leaves, then empties.  Planes round the padded f32 boxes outward onto the
+// 16-bit grid with the 0.1-step margin of QNode2, then outward again onto the node's 6-bit frame,
+// so culling stays conservative.
+constexpr int kW4Units = 2;  // 16-B units per node
+constexpr int kTriUnits = 3;  // 16-B units per TriRec
+struct alignas(16) QNode4C {
+    uint32_t w[8];
+};
+static_assert(sizeof(QNode4C) == 32, "QNode4C must be 32 B");
+
+// The grid-independent f32 form of a CW4 node, kept on the device so that a new grid re-quantizes
+// every node there (launch_requant_w4): four padded child boxes, the meta bits, the block base and
+// the node's own unit.
+struct alignas(16) W4NodeF {
+    float lo[4][3];
+    float hi[4][3];
+    uint32_t meta;
+    uint32_t base;
+    uint32_t self;
+    uint32_t pad;
+};
+static_assert(sizeof(W4NodeF) == 112, "W4NodeF must be 112 B");
+
 // Stack-entry / child code of an empty child in the coded and quantized nodes (code_nodes,
 // arx_bvh.hpp): a leaf of 0 triangles (-1 is kept free: it means "no entry").
 constexpr int32_t kEmptyChildCode = ~16;
@@ -99,6 +134,12 @@ struct TraceArgs {
     int32_t delay;
     int32_t is_mono;
     int32_t bvh_depth;   // inner levels on the longest root path (top node included) = max stack use
+    unsigned long long* prof;  // per-wave records of a profiling build (ARX_TRACE_PROF); null otherwise
+    const void* wbuf;          // CW4 buffer (nodes + leaf triangles, 16-B units); null: a BVH2 path
 };
+// Node formats of the trace kernel (arx_stats::trace_format)
+constexpr int kFmtF32 = 0, kFmtQ16 = 1, kFmtW4 = 2;
+// Per-wave record of a profiling build (ARX_TRACE_PROF=1, arx_debug_trace_profile): u64 words
+constexpr int kProfWords = 16;
 
 }  // namespace arx

@@ -19,6 +19,7 @@
 
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
+#include "arx_wide.hpp"
 
 namespace arx {
 namespace {
@@ -195,6 +196,71 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
         child_box(a.root_ref, a.root_count, lo, hi);
         write_child(a, inv, 0, 1, lo, hi, child_code(a.root_ref, a.root_count), a.root_count < 0);
     }
+    if (!a.wbuf) return;
+    // 4. the CW4 copy: every receiver CW4 node from the refit boxes of its BVH2 children (padded as
+    //    the coded nodes), its leaf triangles, and the top node
+    for (int i = threadIdx.x; i < a.n_w4; i += kRefitThreads) {
+        const int32_t* sd = a.w4_nodes + 11 * i;
+        W4NodeF n;
+        n.meta = (uint32_t)sd[8];
+        n.base = (uint32_t)sd[9];
+        n.self = (uint32_t)sd[10];
+        n.pad = 0u;
+        for (int c = 0; c < 4; ++c) {
+            float lo[3], hi[3];
+            child_box(sd[2 * c], sd[2 * c + 1], lo, hi);
+            for (int k = 0; k < 3; ++k) {
+                n.lo[c][k] = lo[k] - a.pad;
+                n.hi[c][k] = hi[k] + a.pad;
+            }
+        }
+        QNode4C q;
+        if (!quantize_w4(n, a.grid, q)) atomicOr(a.flag, 1u);
+        a.wbuf[n.self] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
+        a.wbuf[n.self + 1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
+    }
+    for (int i = threadIdx.x; i < a.n_w4_tris; i += kRefitThreads) {
+        const uint32_t unit = (uint32_t)a.w4_tris[2 * i];
+        const int32_t t = a.w4_tris[2 * i + 1];
+        const TriRec src = a.local_tris[t];
+        const float* v = wv + 9 * t;
+        a.wbuf[unit] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                  __float_as_uint(src.absorption));
+        a.wbuf[unit + 1] = make_uint4(__float_as_uint(v[3]), __float_as_uint(v[4]), __float_as_uint(v[5]), (uint32_t)src.id);
+        a.wbuf[unit + 2] = make_uint4(__float_as_uint(v[6]), __float_as_uint(v[7]), __float_as_uint(v[8]), (uint32_t)src.pad);
+    }
+    if (threadIdx.x == 0) {
+        W4NodeF n;
+        n.meta = (a.scene_nonempty ? 1u : 0u) | (a.root_count >= 0 ? 1u << 2 : 0u);
+        n.base = 2u;
+        n.self = 0u;
+        n.pad = 0u;
+        float lo[3], hi[3];
+        child_box(a.root_ref, a.root_count, lo, hi);
+        for (int k = 0; k < 3; ++k) {
+            n.lo[0][k] = a.scene_lo[k];
+            n.hi[0][k] = a.scene_hi[k];
+            n.lo[1][k] = lo[k] - a.pad;
+            n.hi[1][k] = hi[k] + a.pad;
+            n.lo[2][k] = n.lo[3][k] = 0.0f;
+            n.hi[2][k] = n.hi[3][k] = 0.0f;
+        }
+        QNode4C q;
+        if (!quantize_w4(n, a.grid, q)) atomicOr(a.flag, 1u);
+        a.wbuf[0] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
+        a.wbuf[1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
+    }
+}
+
+__global__ __launch_bounds__(256) void requant_w4_kernel(const W4NodeF* __restrict__ nodes, uint64_t n, QGrid g,
+                                                          uint4* __restrict__ wbuf, unsigned int* flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const W4NodeF nd = nodes[i];
+    QNode4C q;
+    if (!quantize_w4(nd, g, q)) atomicOr(flag, 1u);
+    wbuf[nd.self] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
+    wbuf[nd.self + 1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
 }
 
 // One quantized child: quantize_nodes16 (arx_bvh.cpp) on the device.  The f64 division is IEEE
@@ -239,6 +305,15 @@ __global__ __launch_bounds__(256) void requant16_kernel(const BvhNode* __restric
 }
 
 }  // namespace
+
+hipError_t launch_requant_w4(const W4NodeF* nodes, uint64_t n, const QGrid& g, uint4* wbuf, unsigned int* flag,
+                             hipStream_t s) {
+    (void)hipGetLastError();
+    if (n == 0) return hipSuccess;
+    if (!nodes || !wbuf || !flag) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(requant_w4_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, g, wbuf, flag);
+    return hipGetLastError();
+}
 
 hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
                             hipStream_t s) {

@@ -209,10 +209,12 @@ __device__ __forceinline__ bool tri_test(const Ray& r, float4 p0, float4 p1, flo
     return true;
 }
 
-__device__ __forceinline__ void leaf_hits(const TriRec* __restrict__ tris, const Ray& r, int first, int count,
+// Triangles [unit, unit + 3*count) of a 16-B-unit array (TriRec = 3 units): d_tris for the BVH2
+// trees, the CW4 buffer's leaf blocks for CW4.  best = the closest hit's unit.
+__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count,
                                           float& best_t, int& best_id, int& best) {
     for (int k = 0; k < count; ++k) {
-        const float4* tp = reinterpret_cast<const float4*>(tris + first + k);
+        const float4* tp = base + unit + 3 * k;
         const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
         Hit h;
         if (tri_test(r, p0, p1, p2, h)) {
@@ -220,7 +222,7 @@ __device__ __forceinline__ void leaf_hits(const TriRec* __restrict__ tris, const
             if (h.t < best_t || (h.t == best_t && id < best_id)) {
                 best_t = h.t;
                 best_id = id;
-                best = first + k;
+                best = unit + 3 * k;
             }
         }
     }
@@ -261,14 +263,14 @@ __device__ __forceinline__ void ray_init(const TraceArgs& a, RayState& s, uint64
 
 // __closesthit__radiance (devicePrograms.cu:62-180) for TriRec `hit`, or __miss__radiance
 // (:186-190) when hit < 0.  r is the ray the query was traced with.
-__device__ __forceinline__ void shade(const TraceArgs& a, RayState& s, const Ray& r, int hit, uint32_t& n_rx,
-                                      uint32_t& n_miss) {
+__device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restrict__ tbase, RayState& s, const Ray& r,
+                                      int hit, uint32_t& n_rx, uint32_t& n_miss) {
     if (hit < 0) {
         ++n_miss;
         s.depth = -1;
         return;
     }
-    const float4* tp = reinterpret_cast<const float4*>(a.tris + hit);
+    const float4* tp = tbase + hit;  // hit = the triangle's 16-B unit (leaf_hits)
     const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
     const float3 P1 = make_float3(p0.x, p0.y, p0.z);
     const float3 P2 = make_float3(p1.x, p1.y, p1.z);
@@ -367,6 +369,7 @@ template <int BLOCK, int ROWS>
 struct LdsStack {
     int* base;  // &stk[lane]
     __device__ __forceinline__ int& at(int slot) const { return base[slot * BLOCK]; }
+    __device__ __forceinline__ int read(int slot) const { return base[slot * BLOCK]; }
     __device__ __forceinline__ int rows() const { return ROWS; }
 };
 struct GlobalStack {
@@ -374,6 +377,7 @@ struct GlobalStack {
     uint64_t stride;
     int nrows;
     __device__ __forceinline__ int& at(int slot) const { return base[(uint64_t)slot * stride]; }
+    __device__ __forceinline__ int read(int slot) const { return base[(uint64_t)slot * stride]; }
     __device__ __forceinline__ int rows() const { return nrows; }
 };
 
@@ -392,9 +396,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p) {
 //        origins on the grid, far below the 0.1-step outward margin of every quantized plane
 //        (quantize_nodes16; the launcher checks the emitter is on the grid).
 //   f32: the coded BvhNode (56 of its 64 B), ix = inv, oix = o*inv.
-template <bool Q16, typename Stack>
+template <int FMT, typename Stack>
 __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
                                           __amdgpu_buffer_rsrc_t rs) {
+    constexpr bool Q16 = FMT == kFmtQ16;
     // the pop candidate is read first, so its latency hides under the node fetch (slot sp - 1 is
     // not touched by this step's write to slot sp)
     const int sp = t.sp;
@@ -445,14 +450,116 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
 }
 
-// Leaf step: test the pending leaf's triangles, then pop the next entry.
+// CW4 step (arx_layout.hpp): one 32-B node = two 16-B loads for four children.  Plane q of axis k
+// is 4*o_k + q*2^e_k grid quanta, so t = fma(q, ix*2^e, fma(o, 4*ix, -oix)) (ix*2^e exact): the
+// Q16 slab arithmetic with the frame folded in.  The hit children are sorted by entry distance
+// (a 5-exchange network), the nearest is taken and the others are pushed farthest first.  Up to
+// three pushes per step: the stack rows above ROWS live in the global overflow column (deep
+// trees; the hot path never touches it while every lane's stack stays below ROWS - 3).
+__device__ __forceinline__ void cas(float& ka, int& va, float& kb, int& vb) {
+    const bool sw = kb < ka;
+    const float k0 = sw ? kb : ka, k1 = sw ? ka : kb;
+    const int v0 = sw ? vb : va, v1 = sw ? va : vb;
+    ka = k0;
+    kb = k1;
+    va = v0;
+    vb = v1;
+}
+
+template <int S>
+__device__ __forceinline__ float w4_plane(const uint32_t (&w)[5]) {
+    return (float)((w[S / 5] >> (6 * (S % 5))) & 63u);
+}
+
+template <int C>
+__device__ __forceinline__ float w4_child(const uint32_t (&w)[5], float sx, float bx, float sy, float by, float sz,
+                                          float bz, float best_t, float& tf_out) {
+    const float x0 = __builtin_fmaf(w4_plane<6 * C + 0>(w), sx, bx), x1 = __builtin_fmaf(w4_plane<6 * C + 1>(w), sx, bx);
+    const float y0 = __builtin_fmaf(w4_plane<6 * C + 2>(w), sy, by), y1 = __builtin_fmaf(w4_plane<6 * C + 3>(w), sy, by);
+    const float z0 = __builtin_fmaf(w4_plane<6 * C + 4>(w), sz, bz), z1 = __builtin_fmaf(w4_plane<6 * C + 5>(w), sz, bz);
+    tf_out = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), best_t));
+    return fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+}
+
+template <int BLOCK, int ROWS>
+struct W4Stack {
+    int* lds;        // &stk[lane]
+    int* glob;       // &gstack[gid]: rows ROWS.. (overflow)
+    uint64_t stride;
+    __device__ __forceinline__ int read(int slot) const {
+        return slot < ROWS ? lds[slot * BLOCK] : glob[(uint64_t)(slot - ROWS) * stride];
+    }
+    __device__ __forceinline__ void write(int slot, int v) const {
+        if (slot < ROWS) lds[slot * BLOCK] = v;
+        else glob[(uint64_t)(slot - ROWS) * stride] = v;
+    }
+};
+
 template <typename Stack>
-__device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav& t, const Stack& stk) {
-    const int v = ~t.node;
-    leaf_hits(a.tris, r, v >> 4, v & 15, t.best_t, t.best_id, t.best);
+__device__ __forceinline__ void node_step_w4(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
+                                             __amdgpu_buffer_rsrc_t rs) {
     const int sp = t.sp;
     const int sp_pop = max(sp - 1, 0);
-    int top = stk.at(sp_pop);
+    int top = stk.read(sp_pop);
+    const int off = t.node * 16;
+    const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
+    const float sx = __builtin_ldexpf(ix, (int)(A.x >> 28));
+    const float sy = __builtin_ldexpf(iy, (int)((A.y >> 14) & 15u));
+    const float sz = __builtin_ldexpf(iz, (int)((A.y >> 18) & 15u));
+    const float bx = __builtin_fmaf((float)(A.x & 0x3FFFu), 4.0f * ix, -oix);
+    const float by = __builtin_fmaf((float)((A.x >> 14) & 0x3FFFu), 4.0f * iy, -oiy);
+    const float bz = __builtin_fmaf((float)(A.y & 0x3FFFu), 4.0f * iz, -oiz);
+    const uint32_t meta = A.y >> 22;  // bits 30..31 are zero
+    const uint32_t w[5] = {A.z, A.w, B.x, B.y, B.z};
+    const int base = (int)B.w;
+    const float inf = __builtin_huge_valf();
+    float tf0, tf1, tf2, tf3;
+    const float tn0 = w4_child<0>(w, sx, bx, sy, by, sz, bz, t.best_t, tf0);
+    const float tn1 = w4_child<1>(w, sx, bx, sy, by, sz, bz, t.best_t, tf1);
+    const float tn2 = w4_child<2>(w, sx, bx, sy, by, sz, bz, t.best_t, tf2);
+    const float tn3 = w4_child<3>(w, sx, bx, sy, by, sz, bz, t.best_t, tf3);
+    const uint32_t m0 = meta & 3u, m1 = (meta >> 2) & 3u, m2 = (meta >> 4) & 3u, m3 = (meta >> 6) & 3u;
+    float k0 = ((tn0 <= tf0) & (m0 != 0u)) ? tn0 : inf;
+    float k1 = ((tn1 <= tf1) & (m1 != 0u)) ? tn1 : inf;
+    float k2 = ((tn2 <= tf2) & (m2 != 0u)) ? tn2 : inf;
+    float k3 = ((tn3 <= tf3) & (m3 != 0u)) ? tn3 : inf;
+    // child codes: inner slots come first (node at base + 2c), then the leaves' triangles
+    const int i1 = m1 == 1u, i2 = m2 == 1u, i3 = m3 == 1u;
+    const int n_inner = (int)(m0 == 1u) + i1 + i2 + i3;
+    const int l0 = m0 >= 2u ? (int)m0 - 1 : 0, l1 = m1 >= 2u ? (int)m1 - 1 : 0, l2 = m2 >= 2u ? (int)m2 - 1 : 0;
+    const int lb = base + 2 * n_inner;
+    int c0 = m0 == 1u ? base : ~(lb * 4 + l0);
+    int c1 = i1 ? base + 2 : ~((lb + 3 * l0) * 4 + l1);
+    int c2 = i2 ? base + 4 : ~((lb + 3 * (l0 + l1)) * 4 + l2);
+    int c3 = i3 ? base + 6 : ~((lb + 3 * (l0 + l1 + l2)) * 4 + (m3 >= 2u ? (int)m3 - 1 : 0));
+    cas(k0, c0, k1, c1);
+    cas(k2, c2, k3, c3);
+    cas(k0, c0, k2, c2);
+    cas(k1, c1, k3, c3);
+    cas(k1, c1, k2, c2);
+    const int hits = (int)(k0 < inf) + (int)(k1 < inf) + (int)(k2 < inf) + (int)(k3 < inf);
+    // pushes above the top (the farthest deepest): hits 4 -> c3 c2 c1, 3 -> c2 c1, 2 -> c1
+    stk.write(sp, hits == 4 ? c3 : (hits == 3 ? c2 : c1));
+    stk.write(sp + 1, hits == 4 ? c2 : c1);
+    stk.write(sp + 2, c1);
+    asm volatile("" : "+v"(top));
+    const int popped = sp > 0 ? top : -1;
+    t.node = hits > 0 ? c0 : popped;
+    t.sp = hits > 0 ? sp + hits - 1 : sp_pop;
+}
+
+// Leaf step: test the pending leaf's triangles, then pop the next entry.
+// BVH2 leaf codes ~(first*16 + count) (first = TriRec index); CW4 leaf codes ~(unit*4 + count).
+template <int FMT, typename Stack>
+__device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, const Ray& r, Trav& t, const Stack& stk) {
+    const int v = ~t.node;
+    if constexpr (FMT == kFmtW4) leaf_hits(tbase, r, v >> 2, v & 3, t.best_t, t.best_id, t.best);
+    else leaf_hits(tbase, r, 3 * (v >> 4), v & 15, t.best_t, t.best_id, t.best);
+    const int sp = t.sp;
+    const int sp_pop = max(sp - 1, 0);
+    int top = stk.read(sp_pop);
     asm volatile("" : "+v"(top));
     t.node = sp > 0 ? top : -1;
     t.sp = sp_pop;
@@ -468,6 +575,9 @@ __device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav
 #endif
 #ifndef ARX_TRACE_COUNT
 #define ARX_TRACE_COUNT 0  // 1: count node steps / leaf triangle tests into counters[4..5]
+#endif
+#ifndef ARX_TRACE_PROF
+#define ARX_TRACE_PROF 0  // 1: per-wave timing and lane-occupancy records into TraceArgs::prof
 #endif
 #if ARX_TRACE_WAVES == 5
 #define ARX_TRACE_VGPR_FENCE "v87"
@@ -485,8 +595,10 @@ __device__ __forceinline__ void leaf_step(const TraceArgs& a, const Ray& r, Trav
 // loop: NSTEPS guarded node steps per iteration; leaves are postponed and intersected wave-wide
 // once LEAF_THRESH lanes hold one (or no lane can step); the loop is left when THRESH lanes wait
 // for shading.
-template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, bool Q16, bool GSTACK>
+template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT, bool GSTACK>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
+    constexpr bool Q16 = FMT == kFmtQ16;
+    constexpr bool W4 = FMT == kFmtW4;
     __shared__ int stk_lds[GSTACK ? 1 : kLdsStack * BLOCK];
     // Hold the VGPR allocation at the count that fits exactly MINW waves per SIMD (see
     // ARX_TRACE_VGPR_FENCE): the kernel needs ~74, which would let the dispatcher put 6 waves on
@@ -494,16 +606,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     asm volatile("" ::: ARX_TRACE_VGPR_FENCE);
     const int lane = threadIdx.x;
     const uint32_t gid = blockIdx.x * BLOCK + threadIdx.x;
-    using Stack = typename std::conditional<GSTACK, GlobalStack, LdsStack<BLOCK, kLdsStack>>::type;
+    using Stack = typename std::conditional<
+        W4, W4Stack<BLOCK, kLdsStack>,
+        typename std::conditional<GSTACK, GlobalStack, LdsStack<BLOCK, kLdsStack>>::type>::type;
     Stack stk;
-    if constexpr (GSTACK) {
+    if constexpr (W4) {  // LDS rows, then the global overflow column
+        stk.lds = stk_lds + lane;
+        stk.glob = a.gstack + gid;
+        stk.stride = a.gstack_lanes;
+    } else if constexpr (GSTACK) {
         stk.base = a.gstack + gid;
         stk.stride = a.gstack_lanes;
         stk.nrows = a.bvh_depth + 1;
     } else {
         stk.base = stk_lds + lane;
     }
-    const __amdgpu_buffer_rsrc_t nrs = Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes);
+    const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf) : (Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes));
+    const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
     const uint64_t n = a.ray_end - a.ray_begin;
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane(gid >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
@@ -512,6 +631,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
 #if ARX_TRACE_COUNT  // measurement builds only (build.py --exp ... -D ARX_TRACE_COUNT=1)
     uint32_t n_steps = 0, n_tris = 0;
+#endif
+#if ARX_TRACE_PROF  // measurement builds only: wave-uniform tallies (popcounts of ballots)
+    // [0] start [1] end [2] rays [3] queries [4] node-step slots run [5] node lane-steps [6] leaf
+    // phases [7] leaf lanes [8] shade phases [9] shade lanes [10] outer iterations [11] inner
+    // iterations [12] time the wave's ray range ran out [13] wave id [14] refill phases [15] -
+    uint64_t pf[kProfWords] = {};
+    pf[0] = __builtin_readcyclecounter();
+    pf[13] = wave_id;
 #endif
     bool active = false, trav = false, exhausted = w_next >= w_end;
     RayState s;
@@ -525,11 +652,28 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     t.sp = 0;
     float oix = 0.f, oiy = 0.f, oiz = 0.f;
     while (true) {
+#if ARX_TRACE_PROF
+        ++pf[10];
+        {
+            const unsigned long long sh = __ballot(active && !trav);
+            if (sh) {
+                ++pf[8];
+                pf[9] += __popcll(sh);
+            }
+        }
+#endif
         if (active && !trav) {
-            shade(a, s, r, t.best, n_rx, n_miss);
+            shade(a, tbase, s, r, t.best, n_rx, n_miss);
             if (!wants_query(a, s)) active = false;
         }
         const unsigned long long need = __ballot(!active);
+#if ARX_TRACE_PROF
+        if (need != 0ull && !exhausted) {
+            ++pf[14];
+            pf[2] += std::min<uint64_t>(__popcll(need), w_end - w_next);
+            if (w_next + __popcll(need) >= w_end) pf[12] = __builtin_readcyclecounter();
+        }
+#endif
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
             const uint64_t base = w_next;
@@ -548,7 +692,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
         if (active && !trav) {
             ++n_q;
             setup_ray(r, s.pos, s.dir);
-            if constexpr (Q16) {  // grid form of the slab planes (node_step)
+            if constexpr (Q16 || W4) {  // grid form of the slab planes (node_step, node_step_w4)
                 oix = (r.o[0] - a.qgrid.origin[0]) * r.inv[0];
                 oiy = (r.o[1] - a.qgrid.origin[1]) * r.inv[1];
                 oiz = (r.o[2] - a.qgrid.origin[2]) * r.inv[2];
@@ -563,7 +707,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             t.best_t = __builtin_huge_valf();
             t.best_id = 0x7fffffff;
             t.best = -1;
-            t.node = 0;
+            t.node = 0;  // the top node (node 0; unit 0 of the CW4 buffer)
             t.sp = 0;
             trav = true;
         }
@@ -577,23 +721,55 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             const unsigned long long m_leaf = __ballot(t.node <= -2);
             if ((m_node | m_leaf) == 0ull) break;
             if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+#if ARX_TRACE_PROF
+            ++pf[11];
+#endif
             if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
 #pragma unroll
-                for (int k = 0; k < NSTEPS; ++k)
+                for (int k = 0; k < NSTEPS; ++k) {
+#if ARX_TRACE_PROF
+                    const unsigned long long mk = __ballot(t.node >= 0);
+                    if (mk) {
+                        ++pf[4];
+                        pf[5] += __popcll(mk);
+                    }
+#endif
                     if (t.node >= 0) {
 #if ARX_TRACE_COUNT
                         ++n_steps;
 #endif
-                        node_step<Q16>(r, oix, oiy, oiz, t, stk, nrs);
+                        if constexpr (W4) node_step_w4(r, oix, oiy, oiz, t, stk, nrs);
+                        else node_step<FMT>(r, oix, oiy, oiz, t, stk, nrs);
                     }
-            } else if (t.node <= -2) {
-#if ARX_TRACE_COUNT
-                n_tris += (uint32_t)((~t.node) & 15);
+                }
+            } else {
+#if ARX_TRACE_PROF
+                ++pf[6];
+                pf[7] += __popcll(m_leaf);
 #endif
-                leaf_step(a, r, t, stk);
+                if (t.node <= -2) {
+#if ARX_TRACE_COUNT
+                    n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
+#endif
+                    leaf_step<FMT>(tbase, r, t, stk);
+                }
             }
         }
     }
+#if ARX_TRACE_PROF
+    {
+        unsigned int vq = n_q;
+        for (int off = 32; off > 0; off >>= 1) vq += __shfl_xor(vq, off, 64);
+        pf[3] = vq;
+        pf[1] = __builtin_readcyclecounter();
+        // one word per lane (a vector store with per-lane addresses)
+        const int l = lane & 63;
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < kProfWords; ++k) v = (l == k) ? pf[k] : v;
+        if (a.prof && l < kProfWords) a.prof[(uint64_t)wave_id * kProfWords + l] = v;
+    }
+#endif
     flush_counters(a, n_q, n_rx, n_miss, lane);
 #if ARX_TRACE_COUNT  // [4] node steps, [5] leaf triangle tests (lane level)
     atomicAdd(a.counters + 4, (unsigned long long)n_steps);
@@ -664,9 +840,9 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
 constexpr int kSimdsPerCu = 4;
 
-template <bool Q16, bool GSTACK>
+template <int FMT, bool GSTACK>
 hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
-    auto k = trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, Q16, GSTACK>;
+    auto k = trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>;
     const uint64_t n_rays = args.ray_end - args.ray_begin;
     // persistent grid: exactly kWaves waves per SIMD on every CU, fewer blocks for small launches
     // (one ray per lane)
@@ -678,7 +854,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
 #endif
     const uint64_t want = (n_rays + kBlock - 1) / kBlock;
     uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
-    if (GSTACK) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
+    if (GSTACK || FMT == kFmtW4) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
     const int grid = (int)std::max<uint64_t>(1, std::min(want, cap));
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)));
@@ -692,19 +868,24 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_g
     if (a.ray_end <= a.ray_begin) return hipSuccess;
     (void)hipGetLastError();  // report this launch's error, not a stale one of an earlier runtime call
     if (!a.dirs || !a.cnodes || !a.tris || !a.hist || !a.counters) return hipErrorInvalidValue;
+    if (a.wbuf) {  // CW4: LDS rows + a global overflow column per lane (W4Stack)
+        if (!a.gstack || a.gstack_lanes < (uint64_t)kBlock) return hipErrorInvalidValue;
+        return launch<kFmtW4, false>(a, cus, s);
+    }
     const bool gstack = force_global_stack || a.bvh_depth + 1 > kLdsStack;
     if (gstack && (!a.gstack || a.gstack_lanes < (uint64_t)kBlock)) return hipErrorInvalidValue;
-    if (a.qnodes) return gstack ? launch<true, true>(a, cus, s) : launch<true, false>(a, cus, s);
-    return gstack ? launch<false, true>(a, cus, s) : launch<false, false>(a, cus, s);
+    if (a.qnodes) return gstack ? launch<kFmtQ16, true>(a, cus, s) : launch<kFmtQ16, false>(a, cus, s);
+    return gstack ? launch<kFmtF32, true>(a, cus, s) : launch<kFmtF32, false>(a, cus, s);
 }
 
-hipError_t trace_kernel_occupancy(bool q16, int* vgprs, int* waves_admitted, int* waves_target) {
+hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;
-    const hipError_t e =
-        q16 ? hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
-                                            trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, true, false>))
-            : hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
-                                            trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, false, false>));
+    const void* k =
+        fmt == kFmtW4 ? reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtW4, false>)
+        : fmt == kFmtQ16
+            ? reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtQ16, false>)
+            : reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtF32, false>);
+    const hipError_t e = hipFuncGetAttributes(&fa, k);
     if (e != hipSuccess) return e;
     // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8
     const int alloc = (fa.numRegs + 7) / 8 * 8;

@@ -67,7 +67,7 @@ def bytes_per_bounce(n_tris: int) -> int:
 
 
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
-NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2"}  # arx_stats.trace_format
+NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2", 2: "4-wide compressed (CW4)"}  # arx_stats.trace_format
 
 
 # ----------------------------------------------------------------------------- rank plumbing ---

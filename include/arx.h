@@ -73,7 +73,8 @@ typedef struct arx_stats {
     int32_t trace_vgprs;
     int32_t trace_waves_per_simd;
     int32_t trace_waves_target;
-    int32_t trace_format;    /* node format of the last trace launch: 0 f32, 1 16-bit quantized */
+    int32_t trace_format;    /* node format of the last trace launch: 0 f32 BVH2, 1 16-bit quantized BVH2,
+                              * 2 4-wide compressed (CW4) */
 } arx_stats;
 
 const char* arx_status_string(arx_status s);
@@ -297,12 +298,28 @@ arx_status arx_debug_scene_roundtrip(const float* tri_vertices, const float* tri
  * device re-quantizations issued so far into *requants. */
 arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, size_t n_nodes, float* grid,
                                  uint64_t* requants);
+/* Host only: build the scene, its 16-bit quantized BVH2 and its 4-wide compressed copy (CW4), and
+ * trace n_rays random rays from the emitter through `bounces` specular reflections on the CPU with
+ * both traversals (nearest first, f64 slab and triangle tests); out[16]: [0] queries, [1] / [2]
+ * BVH2 node steps / triangle tests per query, [3] / [4] the same for CW4, [5] CW4 max stack depth,
+ * [6] queries whose two closest hits differ, [7] CW4 nodes, [8] CW4 depth, [9] BVH2 nodes, [10]
+ * BVH2 depth, [11] quantization failures, [12] misses, [13] CW4 99.9th-percentile stack depth,
+ * [14] CW4 buffer units. */
+arx_status arx_debug_wide_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
+                                const float* emitter, int64_t n_rays, int32_t bounces, uint64_t seed, double* out,
+                                size_t n_out);
+/* Profiling builds only (ARX_TRACE_PROF=1, tools/trace_profile.py): the last trace launch's
+ * per-wave records, 16 uint64 per wave (start / end shader clock, rays, queries, node-step slots
+ * and lane-steps, leaf phases and lanes, shade phases and lanes, loop iterations, the time the
+ * wave's ray range ran out, wave id); ARX_ERR_NOT_READY in the product build. */
+arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_words, size_t* n_out);
 /* Raw device counters of the last trace (n <= 8): [0] queries [1] receiver hits [2] misses. */
 arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
-/* Force the trace kernel's fallback paths (parity tests of the paths real scenes rarely take):
- * bit 0 = f32 coded nodes instead of the 16-bit quantized ones (taken automatically while the
- * emitter is off the quantization grid), bit 1 = the global-memory traversal stack (taken
- * automatically for trees deeper than the LDS stack); 0 = automatic. */
+/* Force the trace kernel's other paths (parity tests of the paths real scenes rarely take): the
+ * default is the 4-wide compressed tree (CW4); bit 2 = the 16-bit quantized BVH2 instead, bit 0 =
+ * the f32 coded BVH2 (taken automatically while the emitter is off the quantization grid), bit 1 =
+ * the BVH2 with the global-memory traversal stack (taken automatically for BVH2 trees deeper than
+ * the LDS stack); 0 = automatic. */
 arx_status arx_debug_set_trace_path(arx_renderer* r, int path);
 
 /* ---- Input formats (host only, no device needed) ------------------------------------------ */

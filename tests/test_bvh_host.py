@@ -97,3 +97,42 @@ def test_threaded_build_is_deterministic(tmp_path):
             for _ in range(2)]
     assert int(outs[0][2]) > 8 * 4096 // 4, outs  # big enough for the threaded top levels
     assert outs[0][0] == outs[0][1] == outs[1][0] == outs[1][1], outs
+
+
+def wide_stats(tri_v, tri_abs, emitter, n_rays=400, bounces=8, seed=5):
+    """arx_debug_wide_stats: the BVH2 (16-bit quantized) and its 4-wide compressed copy (CW4)
+    traversed on the CPU over the same bouncing rays."""
+    import ctypes as C
+
+    from audiorenderingv2_amd import _lib
+
+    tv = np.ascontiguousarray(tri_v, np.float32)
+    ta = np.ascontiguousarray(tri_abs, np.float32)
+    em = np.asarray(emitter, np.float32)
+    out = np.zeros(16)
+    _lib.check(_lib.lib().arx_debug_wide_stats(_lib.fptr(tv), _lib.fptr(ta), ta.size, _lib.fptr(em), n_rays, bounces,
+                                               seed, out.ctypes.data_as(C.POINTER(C.c_double)), 16))
+    return dict(zip(["queries", "q2_steps", "q2_tris", "q4_steps", "q4_tris", "q4_max_stack", "mismatches",
+                     "q4_nodes", "q4_depth", "q2_nodes", "q2_depth", "quantize_failures", "misses"], out))
+
+
+@pytest.mark.parametrize("which", ["c1", "cylinders", "soup"])
+def test_cw4_collapse_finds_the_same_closest_hits(which, c1_scene):
+    """The CW4 copy (BVH2 collapsed to 4 children, 6-bit planes on per-node frames, arx_wide.cpp)
+    finds the BVH2's closest hit for every query, quantizes every node onto the grid, and takes
+    fewer node steps than the BVH2."""
+    rng = np.random.default_rng(11)
+    if which == "c1":
+        tv, ta, em = c1_scene.tri_v, c1_scene.tri_abs, (0.5, 3.0, 1.0)
+    elif which == "cylinders":
+        tv = cylinders_scene().reshape(-1, 9)
+        ta, em = np.full(len(tv), 0.3, np.float32), tuple(tv.reshape(-1, 3).mean(0))
+    else:  # a closed box of random triangles, some degenerate
+        tv = rng.uniform(-5, 5, (3000, 9)).astype(np.float32)
+        tv[::17, 3:6] = tv[::17, 0:3]  # zero-area triangles
+        ta, em = np.full(len(tv), 0.2, np.float32), (0.1, 0.2, 0.3)
+    st = wide_stats(tv, ta, em)
+    assert st["queries"] > 400
+    assert st["mismatches"] == 0 and st["quantize_failures"] == 0
+    assert st["q4_steps"] < st["q2_steps"]
+    assert st["q4_depth"] < st["q2_depth"] + 2

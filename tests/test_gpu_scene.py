@@ -93,7 +93,7 @@ def test_walk_off_the_grid_requantizes_on_the_device(conference):
             f.close()
             break
     assert grown_at is not None, "the walk never left the grid"
-    assert r.stats()["trace_format"] == 1  # still on the quantized nodes
+    assert r.stats()["trace_format"] == 2  # still on the quantized (CW4) nodes
     r.close()
 
 

@@ -26,6 +26,8 @@ s = RenderSettings(rays=rays, sample_rate=48000, base_power=3.62, max_bounces=in
 r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
 r.setEmitterPosInOptix(CONFERENCE_EMITTER)
 r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path: 0 CW4 (default), 4 BVH2 16-bit, 1 BVH2 f32
+    r.set_trace_path(int(os.environ["TRACE_PATH"]))
 ms = [r.render() for _ in range(n)]
 st = r.stats()
 irl, irr = r.get_ir()
@@ -37,5 +39,5 @@ if os.environ.get("ARX_GUARD_OUT"):
                    "tree_hash": f"{int(st['tree_hash']):016x}", "trace_vgprs": int(st["trace_vgprs"]),
                    "trace_format": int(st["trace_format"])}, fh)
 print(f"trace {med:.3f} ms (median of {max(n - 1, 1)}) queries {st['queries']} nodes {st['n_nodes']} "
-      f"depth {st['bvh_depth']} ir_checksum {chk} lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}",
+      f"depth {st['bvh_depth']} format {st['trace_format']} vgprs {st['trace_vgprs']} ir_checksum {chk} lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}",
       flush=True)
