@@ -820,7 +820,7 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     if ((e = hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&r->d_counters, kCounters * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc(&r->d_counters, (kCursor + 1) * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc(&r->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
@@ -1012,6 +1012,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     a.tris = r->d_tris;
     a.hist = r->hist();
     a.counters = r->d_counters;
+    a.cursor = r->d_counters + kCursor;
     a.seed = c.seed;
     a.ray_begin = ray_begin;
     a.ray_end = ray_end;

@@ -28,8 +28,10 @@ arx_status fail(arx_status s, const char* fmt, ...) __attribute__((format(printf
     } while (0)
 
 // device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4..5] counting builds
-// [6] receiver refit left the quantization grid
+// [6] receiver refit left the quantization grid [7] unused; the trace launch's ray-pool cursor
+// lives after them (kCursor, reset by each launch itself)
 constexpr int kCounters = 8;
+constexpr int kCursor = 8;
 // receivers up to this many triangles (and whose refit fits one workgroup's LDS: 9 floats per
 // triangle, 11 words per node) are moved by the device refit; larger ones are rebuilt on the host
 // per move

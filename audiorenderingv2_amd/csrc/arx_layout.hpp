@@ -136,6 +136,7 @@ struct TraceArgs {
     int32_t bvh_depth;   // inner levels on the longest root path (top node included) = max stack use
     unsigned long long* prof;  // per-wave records of a profiling build (ARX_TRACE_PROF); null otherwise
     const void* wbuf;          // CW4 buffer (nodes + leaf triangles, 16-B units); null: a BVH2 path
+    unsigned long long* cursor;  // the launch's ray-pool cursor (reset by the direction pre-pass)
 };
 // Node formats of the trace kernel (arx_stats::trace_format)
 constexpr int kFmtF32 = 0, kFmtQ16 = 1, kFmtW4 = 2;

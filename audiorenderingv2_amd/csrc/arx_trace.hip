@@ -576,6 +576,15 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
 #ifndef ARX_TRACE_COUNT
 #define ARX_TRACE_COUNT 0  // 1: count node steps / leaf triangle tests into counters[4..5]
 #endif
+// Dynamic tail: kDynShare/256 of a launch's rays go to the chunk pool (trace_kernel), kDynChunk
+// rays per pool atomic.
+#ifndef ARX_TRACE_DYN_SHARE
+#define ARX_TRACE_DYN_SHARE 0
+#endif
+#ifndef ARX_TRACE_DYN_CHUNK
+#define ARX_TRACE_DYN_CHUNK 64
+#endif
+constexpr int kDynShare = ARX_TRACE_DYN_SHARE, kDynChunk = ARX_TRACE_DYN_CHUNK;
 #ifndef ARX_TRACE_PROF
 #define ARX_TRACE_PROF 0  // 1: per-wave timing and lane-occupancy records into TraceArgs::prof
 #endif
@@ -626,8 +635,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     const uint64_t n = a.ray_end - a.ray_begin;
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane(gid >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
-    uint64_t w_next = n * wave_id / n_waves;
-    const uint64_t w_end = n * (wave_id + 1) / n_waves;
+    // Rays [0, n_static) are dealt out statically (one contiguous range per wave); the rest form a
+    // pool handed out in chunks of kDynChunk rays, one atomic per chunk, to waves whose static range
+    // has run out -- equal work per wave still leaves waves finishing at different times (their
+    // SIMD, CU and XCD neighbours differ), and the pool lets the fast ones finish the launch.
+    const uint64_t n_dyn = (n * (uint64_t)kDynShare) >> 8;
+    const uint64_t n_static = n - n_dyn;
+    uint64_t w_next = n_static * wave_id / n_waves;
+    uint64_t w_end = n_static * (wave_id + 1) / n_waves;
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
 #if ARX_TRACE_COUNT  // measurement builds only (build.py --exp ... -D ARX_TRACE_COUNT=1)
     uint32_t n_steps = 0, n_tris = 0;
@@ -640,7 +655,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     pf[0] = __builtin_readcyclecounter();
     pf[13] = wave_id;
 #endif
-    bool active = false, trav = false, exhausted = w_next >= w_end;
+    bool active = false, trav = false, exhausted = w_next >= w_end && n_dyn == 0;
     RayState s;
     s.depth = -1;
     Ray r;
@@ -674,6 +689,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             if (w_next + __popcll(need) >= w_end) pf[12] = __builtin_readcyclecounter();
         }
 #endif
+        if (need != 0ull && !exhausted && w_next >= w_end) {  // the static range ran out: a pool chunk
+            unsigned long long c = 0ull;
+            if ((lane & 63) == 0) c = atomicAdd(a.cursor, (unsigned long long)kDynChunk);
+            const uint64_t start = n_static + __builtin_amdgcn_readfirstlane((uint32_t)c) +
+                                   ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c >> 32)) << 32);
+            w_next = start;
+            w_end = start + kDynChunk < n ? start + kDynChunk : n;
+            if (start >= n) exhausted = true;
+        }
         if (need != 0ull && !exhausted) {
             const int cnt = __popcll(need);
             const uint64_t base = w_next;
@@ -687,7 +711,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                     active = wants_query(a, s);
                 }
             }
-            if (w_next >= w_end) exhausted = true;
+            if (w_next >= w_end && n_dyn == 0) exhausted = true;
         }
         if (active && !trav) {
             ++n_q;
@@ -808,8 +832,9 @@ __global__ void clear_kernel(unsigned long long* __restrict__ hist, uint64_t n, 
 }
 
 // Direction pre-pass: float4(dir, 0) for rays [first, first + count).
-__global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out) {
+__global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out, unsigned long long* cursor) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *cursor = 0ull;  // the trace launch's chunk pool (trace_kernel) starts empty-handed
     if (i >= count) return;
     const float3 d = ray_direction(seed, first + i);
     out[i] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -857,7 +882,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     if (GSTACK || FMT == kFmtW4) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
     const int grid = (int)std::max<uint64_t>(1, std::min(want, cap));
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
-                       args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)));
+                       args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
     hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), dyn_lds, s, args);
     return hipGetLastError();
 }
@@ -867,7 +892,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
 hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_global_stack) {
     if (a.ray_end <= a.ray_begin) return hipSuccess;
     (void)hipGetLastError();  // report this launch's error, not a stale one of an earlier runtime call
-    if (!a.dirs || !a.cnodes || !a.tris || !a.hist || !a.counters) return hipErrorInvalidValue;
+    if (!a.dirs || !a.cnodes || !a.tris || !a.hist || !a.counters || !a.cursor) return hipErrorInvalidValue;
     if (a.wbuf) {  // CW4: LDS rows + a global overflow column per lane (W4Stack)
         if (!a.gstack || a.gstack_lanes < (uint64_t)kBlock) return hipErrorInvalidValue;
         return launch<kFmtW4, false>(a, cus, s);

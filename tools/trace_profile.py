@@ -43,6 +43,8 @@ def main() -> int:
     r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
     r.setEmitterPosInOptix(CONFERENCE_EMITTER)
     r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+    if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path (0 CW4, 4 BVH2 16-bit)
+        r.set_trace_path(int(os.environ["TRACE_PATH"]))
     for _ in range(3):  # warm-up, then the measured launch
         r.clear_histogram()
         r.trace_rays(0, traced)
@@ -60,7 +62,7 @@ def main() -> int:
     slots = a[:, 4].sum()
     leaf_ph, shade_ph = a[:, 6].sum(), a[:, 8].sum()
     out = {
-        "workload": name, "rays": traced, "bounces": bounces, "waves": int(a.shape[0]),
+        "workload": name, "trace_path": int(os.environ.get("TRACE_PATH", "0")), "rays": traced, "bounces": bounces, "waves": int(a.shape[0]),
         "trace_ms_hip_events": ms,
         "clock_ticks_per_ms": span / ms,
         "span_ticks": span,
