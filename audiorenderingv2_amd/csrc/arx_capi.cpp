@@ -836,10 +836,10 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     for (int f = 0; f < 3; ++f)
         if ((e = trace_kernel_occupancy(f, &r->occ[f][0], &r->occ[f][1], &r->occ[f][2])) != hipSuccess)
             return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
-    r->stats.trace_vgprs = r->occ[kFmtW4][0];
-    r->stats.trace_waves_per_simd = r->occ[kFmtW4][1];
-    r->stats.trace_waves_target = r->occ[kFmtW4][2];
-    r->stats.trace_format = kFmtW4;
+    r->stats.trace_vgprs = r->occ[kFmtQ16][0];
+    r->stats.trace_waves_per_simd = r->occ[kFmtQ16][1];
+    r->stats.trace_waves_target = r->occ[kFmtQ16][2];
+    r->stats.trace_format = kFmtQ16;
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
@@ -1006,8 +1006,9 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     // grid: the slab arithmetic's error bound assumes origins within the grid's extent
     const float* em = r->emitter;
     a.qnodes = (r->q_valid && !r->force_f32_nodes && qgrid_contains(r->qgrid, em, em)) ? r->d_qnodes : nullptr;
-    // the CW4 tree (the default) on the same condition, unless a BVH2 path is forced
-    a.wbuf = (a.qnodes && !r->force_bvh2 && !r->force_global_stack) ? r->d_wbuf : nullptr;
+    // the CW4 tree on the same condition when asked for (arx_debug_set_trace_path bit 3; measured
+    // 1.9x slower than the BVH2 on C3: DESIGN.md section 6.3)
+    a.wbuf = (a.qnodes && r->use_w4 && !r->force_global_stack) ? r->d_wbuf : nullptr;
     a.qgrid = r->qgrid;
     a.tris = r->d_tris;
     a.hist = r->hist();
@@ -1375,10 +1376,10 @@ arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_word
 }
 
 arx_status arx_debug_set_trace_path(arx_renderer* r, int path) {
-    if (!r || path < 0 || path > 7) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!r || path < 0 || path > 15 || (path & 4)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
     r->force_f32_nodes = (path & 1) != 0;
     r->force_global_stack = (path & 2) != 0;
-    r->force_bvh2 = (path & 4) != 0;
+    r->use_w4 = (path & 8) != 0;
     return ARX_OK;
 }
 

@@ -129,7 +129,7 @@ struct arx_renderer {
     arx::W4Build recv4;
     int32_t* d_recv_w4 = nullptr;  // 11 ints per receiver CW4 node
     int32_t* d_recv_w4_tris = nullptr;
-    bool force_bvh2 = false;       // arx_debug_set_trace_path bit 2
+    bool use_w4 = false;           // arx_debug_set_trace_path bit 3: the CW4 tree
     int32_t depth4 = 0;            // CW4 levels (top node included): bounds the stack (3 per level)
     int32_t occ[3][3] = {};        // per node format: VGPRs, waves admitted, waves targeted
     arx::QGrid qgrid{};

@@ -316,10 +316,11 @@ arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_word
 /* Raw device counters of the last trace (n <= 8): [0] queries [1] receiver hits [2] misses. */
 arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
 /* Force the trace kernel's other paths (parity tests of the paths real scenes rarely take): the
- * default is the 4-wide compressed tree (CW4); bit 2 = the 16-bit quantized BVH2 instead, bit 0 =
- * the f32 coded BVH2 (taken automatically while the emitter is off the quantization grid), bit 1 =
- * the BVH2 with the global-memory traversal stack (taken automatically for BVH2 trees deeper than
- * the LDS stack); 0 = automatic. */
+ * default is the 16-bit quantized BVH2 with the LDS stack; bit 0 = the f32 coded BVH2 (taken
+ * automatically while the emitter is off the quantization grid), bit 1 = the global-memory
+ * traversal stack (taken automatically for trees deeper than the LDS stack), bit 3 = the 4-wide
+ * compressed tree (CW4, arx_layout.hpp: half the node loads per query, twice the VALU; slower on
+ * MI355X, kept as a measured alternative); 0 = automatic. */
 arx_status arx_debug_set_trace_path(arx_renderer* r, int path);
 
 /* ---- Input formats (host only, no device needed) ------------------------------------------ */

@@ -185,11 +185,11 @@ def test_full_size_c3_properties(conference):
     assert np.array_equal(gl, ol) and np.array_equal(gr, orr)
 
 
-# trace paths (arx_debug_set_trace_path): 0 = the default (the 4-wide compressed tree, CW4), 4 =
-# the 16-bit quantized BVH2 (LDS stack), 1 = f32 coded BVH2 nodes (taken while the emitter is off
-# the quantization grid), 2 = the BVH2 with the global-memory stack (taken by BVH2 trees deeper than
-# the LDS stack), 3 = both BVH2 fallbacks
-PATHS = ["0", "4", "1", "2", "3"]
+# trace paths (arx_debug_set_trace_path): 0 = the default (16-bit quantized BVH2, LDS stack), 8 =
+# the 4-wide compressed tree (CW4), 1 = f32 coded BVH2 nodes (taken while the emitter is off the
+# quantization grid), 2 = the global-memory stack (taken by trees deeper than the LDS stack), 3 =
+# both fallbacks
+PATHS = ["0", "8", "1", "2", "3"]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -215,7 +215,7 @@ def test_trace_paths_match_oracle(c1_scene, conference, path):
     assert st["receiver_hits"] > 0
 
 
-@pytest.mark.parametrize("path", ["4", "1", "2", "3"])
+@pytest.mark.parametrize("path", ["8", "1", "2", "3"])
 def test_trace_paths_identical_at_c3_shape(conference, path):
     """The fallback paths produce the default path's histogram bit for bit on a 100 K-ray,
     16-bounce, 48 kHz launch."""
@@ -230,7 +230,7 @@ def test_trace_paths_identical_at_c3_shape(conference, path):
     assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
 
 
-@pytest.mark.parametrize("path", ["0", "4", "2"])
+@pytest.mark.parametrize("path", ["0", "8", "2"])
 def test_quantized_nodes_regrid_and_fallback(c1_scene, path):
     """16-bit quantized nodes (QNode2): the grid covers scene + receiver + emitter at scene load.
     A listener moved off the grid (outside the room) re-grids once (a wider grid, full
@@ -251,7 +251,7 @@ def test_quantized_nodes_regrid_and_fallback(c1_scene, path):
     assert_same_render(r, c1_scene, (2.5, 9.9, 0.0), 0.0, em_far, s)
 
 
-@pytest.mark.parametrize("path", ["0", "4", "1"])
+@pytest.mark.parametrize("path", ["0", "8", "1"])
 @pytest.mark.parametrize("offset", [(1.0e4, -3.0e3, 5.0e3), (-2.5e5, 0.0, 1.0e5)])
 def test_room_far_from_origin(c1_scene, offset, path):
     """The test.obj room, emitter and listener translated far from the origin: f32 slab and

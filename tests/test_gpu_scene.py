@@ -93,7 +93,13 @@ def test_walk_off_the_grid_requantizes_on_the_device(conference):
             f.close()
             break
     assert grown_at is not None, "the walk never left the grid"
-    assert r.stats()["trace_format"] == 2  # still on the quantized (CW4) nodes
+    assert r.stats()["trace_format"] == 1  # still on the quantized nodes
+    r.set_trace_path(8)  # and the CW4 copy, re-made for the new grid too, gives the same IR
+    r.render()
+    c = r.get_ir()
+    assert r.stats()["trace_format"] == 2
+    assert np.array_equal(c[0].view(np.uint32), a[0].view(np.uint32))
+    assert np.array_equal(c[1].view(np.uint32), a[1].view(np.uint32))
     r.close()
 
 

@@ -26,7 +26,7 @@ s = RenderSettings(rays=rays, sample_rate=48000, base_power=3.62, max_bounces=in
 r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
 r.setEmitterPosInOptix(CONFERENCE_EMITTER)
 r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path: 0 CW4 (default), 4 BVH2 16-bit, 1 BVH2 f32
+if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path: 0 BVH2 16-bit (default), 8 CW4, 1 BVH2 f32
     r.set_trace_path(int(os.environ["TRACE_PATH"]))
 ms = [r.render() for _ in range(n)]
 st = r.stats()

@@ -43,7 +43,7 @@ def main() -> int:
     r = AudioRenderer(s, scene=conference_standin(), receiver=receiver_local())
     r.setEmitterPosInOptix(CONFERENCE_EMITTER)
     r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-    if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path (0 CW4, 4 BVH2 16-bit)
+    if os.environ.get("TRACE_PATH"):  # arx_debug_set_trace_path (0 BVH2 16-bit, 8 CW4)
         r.set_trace_path(int(os.environ["TRACE_PATH"]))
     for _ in range(3):  # warm-up, then the measured launch
         r.clear_histogram()
