@@ -137,6 +137,8 @@ struct TraceArgs {
     unsigned long long* prof;  // per-wave records of a profiling build (ARX_TRACE_PROF); null otherwise
     const void* wbuf;          // CW4 buffer (nodes + leaf triangles, 16-B units); null: a BVH2 path
     unsigned long long* cursor;  // the launch's ray-pool cursor (reset by the direction pre-pass)
+    uint32_t dyn_share;          // rays in the pool: n * dyn_share / 256 (set by launch_trace)
+    uint32_t dyn_chunk;          // rays per pool atomic
 };
 // Node formats of the trace kernel (arx_stats::trace_format)
 constexpr int kFmtF32 = 0, kFmtQ16 = 1, kFmtW4 = 2;

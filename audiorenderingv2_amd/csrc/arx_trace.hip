@@ -576,15 +576,20 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
 #ifndef ARX_TRACE_COUNT
 #define ARX_TRACE_COUNT 0  // 1: count node steps / leaf triangle tests into counters[4..5]
 #endif
-// Dynamic tail: kDynShare/256 of a launch's rays go to the chunk pool (trace_kernel), kDynChunk
-// rays per pool atomic.
+// Dynamic tail (launch_trace): launches with at least kDynMinRaysPerWave rays per wave put
+// kDynShare/256 of their rays into the chunk pool of trace_kernel, kDynChunk rays per pool atomic.
+// Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) keep static ranges: there a
+// chunk is a whole wave's work and the pool only lengthens the longest chains.
 #ifndef ARX_TRACE_DYN_SHARE
-#define ARX_TRACE_DYN_SHARE 0
+#define ARX_TRACE_DYN_SHARE 32
 #endif
 #ifndef ARX_TRACE_DYN_CHUNK
 #define ARX_TRACE_DYN_CHUNK 64
 #endif
-constexpr int kDynShare = ARX_TRACE_DYN_SHARE, kDynChunk = ARX_TRACE_DYN_CHUNK;
+#ifndef ARX_TRACE_DYN_MIN
+#define ARX_TRACE_DYN_MIN 96
+#endif
+constexpr int kDynShare = ARX_TRACE_DYN_SHARE, kDynChunk = ARX_TRACE_DYN_CHUNK, kDynMinRaysPerWave = ARX_TRACE_DYN_MIN;
 #ifndef ARX_TRACE_PROF
 #define ARX_TRACE_PROF 0  // 1: per-wave timing and lane-occupancy records into TraceArgs::prof
 #endif
@@ -639,7 +644,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     // pool handed out in chunks of kDynChunk rays, one atomic per chunk, to waves whose static range
     // has run out -- equal work per wave still leaves waves finishing at different times (their
     // SIMD, CU and XCD neighbours differ), and the pool lets the fast ones finish the launch.
-    const uint64_t n_dyn = (n * (uint64_t)kDynShare) >> 8;
+    const uint64_t n_dyn = (n * (uint64_t)a.dyn_share) >> 8;
+    const uint32_t dyn_chunk = a.dyn_chunk;
     const uint64_t n_static = n - n_dyn;
     uint64_t w_next = n_static * wave_id / n_waves;
     uint64_t w_end = n_static * (wave_id + 1) / n_waves;
@@ -691,11 +697,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
 #endif
         if (need != 0ull && !exhausted && w_next >= w_end) {  // the static range ran out: a pool chunk
             unsigned long long c = 0ull;
-            if ((lane & 63) == 0) c = atomicAdd(a.cursor, (unsigned long long)kDynChunk);
+            if ((lane & 63) == 0) c = atomicAdd(a.cursor, (unsigned long long)dyn_chunk);
             const uint64_t start = n_static + __builtin_amdgcn_readfirstlane((uint32_t)c) +
                                    ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c >> 32)) << 32);
             w_next = start;
-            w_end = start + kDynChunk < n ? start + kDynChunk : n;
+            w_end = start + dyn_chunk < n ? start + dyn_chunk : n;
             if (start >= n) exhausted = true;
         }
         if (need != 0ull && !exhausted) {
@@ -881,9 +887,13 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
     if (GSTACK || FMT == kFmtW4) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
     const int grid = (int)std::max<uint64_t>(1, std::min(want, cap));
+    TraceArgs a2 = args;
+    const bool dyn = n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
+    a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
+    a2.dyn_chunk = (uint32_t)kDynChunk;
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), dyn_lds, s, args);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), dyn_lds, s, a2);
     return hipGetLastError();
 }
 
