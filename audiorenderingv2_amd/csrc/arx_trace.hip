@@ -581,10 +581,10 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
 // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) keep static ranges: there a
 // chunk is a whole wave's work and the pool only lengthens the longest chains.
 #ifndef ARX_TRACE_DYN_SHARE
-#define ARX_TRACE_DYN_SHARE 32
+#define ARX_TRACE_DYN_SHARE 128
 #endif
 #ifndef ARX_TRACE_DYN_CHUNK
-#define ARX_TRACE_DYN_CHUNK 64
+#define ARX_TRACE_DYN_CHUNK 16
 #endif
 #ifndef ARX_TRACE_DYN_MIN
 #define ARX_TRACE_DYN_MIN 96

@@ -69,6 +69,11 @@ def main() -> int:
         "wave_duration": {"mean_over_span": float(dur.mean() / span), "median_over_span": float(np.median(dur) / span),
                           "min_over_span": float(dur.min() / span), "max_over_span": float(dur.max() / span),
                           "p10_over_span": float(np.percentile(dur, 10) / span)},
+        # s_memtime counts per XCD (not comparable across waves): durations only
+        "wave_duration_over_max": {"mean": float(dur.mean() / dur.max()), "median": float(np.median(dur) / dur.max()),
+                                   "p10": float(np.percentile(dur, 10) / dur.max()),
+                                   "p90": float(np.percentile(dur, 90) / dur.max()), "min": float(dur.min() / dur.max())},
+        "max_wave_ticks": float(dur.max()),
         "start_skew_over_span": float((t0.max() - t0.min()) / span),
         "after_range_ran_out_over_span": float(np.mean(t1 - exhaust) / span),
         "queries_per_wave": {"mean": float(a[:, 3].mean()), "min": float(a[:, 3].min()), "max": float(a[:, 3].max())},
