@@ -28,6 +28,10 @@
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
 
+#ifndef ARX_TRACE_SIGNSEL
+#define ARX_TRACE_SIGNSEL 0  // 1: per-ray near/far plane selection in the 16-bit node step
+#endif
+
 namespace arx {
 namespace {
 
@@ -125,6 +129,7 @@ struct Ray {
     float inv[3];    // safe reciprocal direction (box test only)
     float sx, sy, sz;
     int kx, ky, kz;
+    uint32_t nsel[3];  // v_perm selectors per axis: near plane into the low half (ARX_TRACE_SIGNSEL)
 };
 
 __device__ __forceinline__ float sel3(float x, float y, float z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
@@ -163,6 +168,9 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
         float v = dd[k];
         if (fabsf(v) < 1e-20f) v = (v < 0.0f) ? -1e-20f : 1e-20f;
         r.inv[k] = __builtin_amdgcn_rcpf(v);
+        // a (lo | hi << 16) plane word: keep for a positive reciprocal (lo is the near plane), swap
+        // the halves for a negative one
+        r.nsel[k] = r.inv[k] >= 0.0f ? 0x03020100u : 0x01000302u;
     }
 }
 
@@ -408,10 +416,11 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
     float4 na, nb, nc;
     int c0, c1;
+    uint4 A = make_uint4(0u, 0u, 0u, 0u), B = A;
     if constexpr (Q16) {
         const int off = t.node * (int)sizeof(QNode2);
-        const uint4 A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        const uint4 B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
         nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
         nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
@@ -426,16 +435,37 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
         c0 = d.x;
         c1 = d.y;
     }
-    const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
-    const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
-    const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
-    const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
-    const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
-    const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
-    const float tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
-    const float tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
-    const float tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
-    const float tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    float tn0, tf0, tn1, tf1;
+    if constexpr (Q16 && ARX_TRACE_SIGNSEL) {
+        // near / far planes picked per ray (the reciprocal's sign) by a byte permute of each plane
+        // word: no min / max per slab.  The fma is monotone in q, so the near plane's t is the
+        // min of the two and the result is the min / max form's, bit for bit; an empty child's
+        // (1, 0) planes come out near > far on either sign.
+        const uint32_t ax = __builtin_amdgcn_perm(A.x, A.x, r.nsel[0]), ay = __builtin_amdgcn_perm(A.y, A.y, r.nsel[1]);
+        const uint32_t az = __builtin_amdgcn_perm(A.z, A.z, r.nsel[2]), bxw = __builtin_amdgcn_perm(B.x, B.x, r.nsel[0]);
+        const uint32_t byw = __builtin_amdgcn_perm(B.y, B.y, r.nsel[1]), bzw = __builtin_amdgcn_perm(B.z, B.z, r.nsel[2]);
+        const float nx0 = __builtin_fmaf((float)(ax & 0xffffu), ix, -oix), fx0 = __builtin_fmaf((float)(ax >> 16), ix, -oix);
+        const float ny0 = __builtin_fmaf((float)(ay & 0xffffu), iy, -oiy), fy0 = __builtin_fmaf((float)(ay >> 16), iy, -oiy);
+        const float nz0 = __builtin_fmaf((float)(az & 0xffffu), iz, -oiz), fz0 = __builtin_fmaf((float)(az >> 16), iz, -oiz);
+        const float nx1 = __builtin_fmaf((float)(bxw & 0xffffu), ix, -oix), fx1 = __builtin_fmaf((float)(bxw >> 16), ix, -oix);
+        const float ny1 = __builtin_fmaf((float)(byw & 0xffffu), iy, -oiy), fy1 = __builtin_fmaf((float)(byw >> 16), iy, -oiy);
+        const float nz1 = __builtin_fmaf((float)(bzw & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(bzw >> 16), iz, -oiz);
+        tn0 = fmaxf(fmaxf(fmaxf(nx0, ny0), nz0), 0.0f);
+        tf0 = fminf(fminf(fminf(fx0, fy0), fz0), t.best_t);
+        tn1 = fmaxf(fmaxf(fmaxf(nx1, ny1), nz1), 0.0f);
+        tf1 = fminf(fminf(fminf(fx1, fy1), fz1), t.best_t);
+    } else {
+        const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
+        const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
+        const float z00 = __builtin_fmaf(nc.x, iz, -oiz), z01 = __builtin_fmaf(nc.y, iz, -oiz);
+        const float x10 = __builtin_fmaf(nb.x, ix, -oix), x11 = __builtin_fmaf(nb.y, ix, -oix);
+        const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
+        const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
+        tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
+        tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+        tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
+        tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+    }
     const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
     const bool near1 = h1 & (!h0 | (tn1 < tn0));
     const int c_near = near1 ? c1 : c0;
@@ -584,7 +614,7 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
 #define ARX_TRACE_DYN_SHARE 128
 #endif
 #ifndef ARX_TRACE_DYN_CHUNK
-#define ARX_TRACE_DYN_CHUNK 16
+#define ARX_TRACE_DYN_CHUNK 8
 #endif
 #ifndef ARX_TRACE_DYN_MIN
 #define ARX_TRACE_DYN_MIN 96
@@ -660,6 +690,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     uint64_t pf[kProfWords] = {};
     pf[0] = __builtin_readcyclecounter();
     pf[13] = wave_id;
+    // HW_REG_HW_ID (wave / SIMD / CU / SE of this wave) | HW_REG_XCC_ID << 32: s_memtime counts per
+    // XCD, so start skews compare waves of one XCD only
+    pf[15] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+             ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32);
 #endif
     bool active = false, trav = false, exhausted = w_next >= w_end && n_dyn == 0;
     RayState s;

@@ -36,6 +36,25 @@ SHAPES = {  # rays of the launch, rays traced, bounces, sample rate
 W = 16  # kProfWords
 
 
+def per_xcd(a: np.ndarray) -> dict:
+    """Start skew and end spread within each XCD (s_memtime is per XCD), in units of the longest
+    wave, and how the wave duration depends on the wave's slot on its SIMD."""
+    xcc = (a[:, 15].astype(np.uint64) >> np.uint64(32)).astype(np.int64) & 0xF
+    hw = (a[:, 15].astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    dur = a[:, 1] - a[:, 0]
+    dmax = dur.max()
+    out = {}
+    for x in sorted(set(xcc.tolist())):
+        m = xcc == x
+        t0, t1 = a[m, 0], a[m, 1]
+        out[str(x)] = {"waves": int(m.sum()), "start_skew": float((t0.max() - t0.min()) / dmax),
+                       "end_spread": float((t1.max() - t1.min()) / dmax),
+                       "span": float((t1.max() - t0.min()) / dmax), "mean_dur": float(dur[m].mean() / dmax)}
+    out["by_wave_slot_mean_dur"] = {str(k): float(dur[(hw & 0xF) == k].mean() / dmax)
+                                    for k in sorted(set((hw & 0xF).tolist()))}
+    return out
+
+
 def main() -> int:
     name = sys.argv[1] if len(sys.argv) > 1 else "c3"
     rays, traced, bounces, sr = SHAPES[name]
@@ -74,6 +93,7 @@ def main() -> int:
                                    "p10": float(np.percentile(dur, 10) / dur.max()),
                                    "p90": float(np.percentile(dur, 90) / dur.max()), "min": float(dur.min() / dur.max())},
         "max_wave_ticks": float(dur.max()),
+        "per_xcd": per_xcd(a),
         "start_skew_over_span": float((t0.max() - t0.min()) / span),
         "after_range_ran_out_over_span": float(np.mean(t1 - exhaust) / span),
         "queries_per_wave": {"mean": float(a[:, 3].mean()), "min": float(a[:, 3].min()), "max": float(a[:, 3].max())},
