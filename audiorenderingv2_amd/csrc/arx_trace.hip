@@ -28,8 +28,11 @@
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
 
+#ifndef ARX_TRACE_PKFMA
+#define ARX_TRACE_PKFMA 0  // 1: packed fma for each slab's plane pair (design experiment)
+#endif
 #ifndef ARX_TRACE_SIGNSEL
-#define ARX_TRACE_SIGNSEL 0  // 1: per-ray near/far plane selection in the 16-bit node step
+#define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
 #endif
 
 namespace arx {
@@ -444,12 +447,24 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
         const uint32_t ax = __builtin_amdgcn_perm(A.x, A.x, r.nsel[0]), ay = __builtin_amdgcn_perm(A.y, A.y, r.nsel[1]);
         const uint32_t az = __builtin_amdgcn_perm(A.z, A.z, r.nsel[2]), bxw = __builtin_amdgcn_perm(B.x, B.x, r.nsel[0]);
         const uint32_t byw = __builtin_amdgcn_perm(B.y, B.y, r.nsel[1]), bzw = __builtin_amdgcn_perm(B.z, B.z, r.nsel[2]);
+#if ARX_TRACE_PKFMA  // near and far plane of one slab in one packed fma (v_pk_fma_f32)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        auto slab = [](uint32_t w, float i, float oi) -> f2 {
+            const f2 q = {(float)(w & 0xffffu), (float)(w >> 16)};
+            return __builtin_elementwise_fma(q, (f2){i, i}, (f2){-oi, -oi});
+        };
+        const f2 sx0 = slab(ax, ix, oix), sy0 = slab(ay, iy, oiy), sz0 = slab(az, iz, oiz);
+        const f2 sx1 = slab(bxw, ix, oix), sy1 = slab(byw, iy, oiy), sz1 = slab(bzw, iz, oiz);
+        const float nx0 = sx0.x, fx0 = sx0.y, ny0 = sy0.x, fy0 = sy0.y, nz0 = sz0.x, fz0 = sz0.y;
+        const float nx1 = sx1.x, fx1 = sx1.y, ny1 = sy1.x, fy1 = sy1.y, nz1 = sz1.x, fz1 = sz1.y;
+#else
         const float nx0 = __builtin_fmaf((float)(ax & 0xffffu), ix, -oix), fx0 = __builtin_fmaf((float)(ax >> 16), ix, -oix);
         const float ny0 = __builtin_fmaf((float)(ay & 0xffffu), iy, -oiy), fy0 = __builtin_fmaf((float)(ay >> 16), iy, -oiy);
         const float nz0 = __builtin_fmaf((float)(az & 0xffffu), iz, -oiz), fz0 = __builtin_fmaf((float)(az >> 16), iz, -oiz);
         const float nx1 = __builtin_fmaf((float)(bxw & 0xffffu), ix, -oix), fx1 = __builtin_fmaf((float)(bxw >> 16), ix, -oix);
         const float ny1 = __builtin_fmaf((float)(byw & 0xffffu), iy, -oiy), fy1 = __builtin_fmaf((float)(byw >> 16), iy, -oiy);
         const float nz1 = __builtin_fmaf((float)(bzw & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(bzw >> 16), iz, -oiz);
+#endif
         tn0 = fmaxf(fmaxf(fmaxf(nx0, ny0), nz0), 0.0f);
         tf0 = fminf(fminf(fminf(fx0, fy0), fz0), t.best_t);
         tn1 = fmaxf(fmaxf(fmaxf(nx1, ny1), nz1), 0.0f);
