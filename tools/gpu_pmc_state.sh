@@ -19,7 +19,7 @@ for v in ${CONFIGS:-prod}; do
              "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum" \
              "TCC_HIT_sum TCC_MISS_sum"}; do
     tag=v${v}_$(echo $grp | cut -d' ' -f1)
-    timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmcs/$tag -o p -- python3 $R/tools/trace_once.py 2 > gpurun_out/pmcs/$tag.log 2>&1
+    ARX_GUARD_OUT=$R/gpurun_out/pmcs/guard_$v.json timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmcs/$tag -o p -- python3 $R/tools/trace_once.py 2 > gpurun_out/pmcs/$tag.log 2>&1
     rc=$?
     echo "$tag rc=$rc" >> gpurun_out/pmcs/status.txt
     if [ $rc -ne 0 ]; then echo "pmc $tag failed rc=$rc"; tail -5 gpurun_out/pmcs/$tag.log; exit 1; fi

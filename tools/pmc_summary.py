@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc csv output of the trace kernel (tools/gpu_pmc_state.sh).
 
-    python tools/pmc_summary.py gpurun_out/pmcs
+    python tools/pmc_summary.py gpurun_out/pmcs [td.json guard.json]
 
 Per variant: every counter averaged per trace-kernel dispatch, plus derived ratios
 (per-CU busy fractions, VALU/SALU per wave-cycle, L2 hit rate, mean L2 read latency).
@@ -8,6 +8,7 @@ Per variant: every counter averaged per trace-kernel dispatch, plus derived rati
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
@@ -32,7 +33,22 @@ def load(root):
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcs"
     cus = 256
-    for variant, c in sorted(load(root).items()):
+    data = load(root)
+    if len(sys.argv) > 3:  # --json: the product variant's TD / TA busy fractions + the run's guard
+        c = data["vprod"]
+        g = c["GRBM_GUI_ACTIVE"] / 8
+        guard = json.load(open(sys.argv[3]))
+        out = {"workload": guard.get("workload"), "tree_hash": guard.get("tree_hash"),
+               "trace_vgprs": guard.get("trace_vgprs"), "kernel": "trace_kernel (16-bit BVH2, LDS stack)",
+               "td_busy_per_cu_cycle": c["TD_TD_BUSY_sum"] / cus / g, "ta_busy_per_cu_cycle": c["TA_TA_BUSY_sum"] / cus / g,
+               "l2_hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]),
+               "sq_wait_any_per_wave_cycle": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
+               "valu_active_per_wave_cycle": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
+               "valu_instructions": c["SQ_INSTS_VALU"],
+               "source": sys.argv[2]}
+        with open(sys.argv[2], "w") as fh:
+            json.dump(out, fh, indent=1)
+    for variant, c in sorted(data.items()):
         print(f"== {variant}")
         for k in sorted(c):
             print(f"  {k:34s} {c[k]:.4g}")

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Vector-memory ceiling of the trace kernel, calibrated on this GPU.
 
-    python tools/vmem_ceiling.py profiles/r02/td_microbench_sizes.log profiles/r02/pmc_state_r02h.txt \
-        profiles/r02/trace_counts_c3.json > profiles/r02/trace_vmem_ceiling.json
+    python tools/vmem_ceiling.py profiles/r02/td_microbench_sizes.log profiles/r03/pmc_state_r03.txt \
+        profiles/r03/trace_counts_c3.json [guard.json] > profiles/r03/trace_vmem_ceiling.json
+
+guard.json (tools/trace_once.py ARX_GUARD_OUT of the PMC run) adds the tree hash and the trace
+kernel's VGPRs, which bench.py checks against its own run.
 
 The trace kernel's node and triangle fetches are divergent 16-B gathers (one 64-B block per lane).
 tools/td_microbench.hip measures the rate of such gathers when they hit in L1 (16 KB table), in
@@ -49,8 +52,10 @@ def main():
     f_l1 = 1.0 - f_l2
     r1, r2, r3 = r[16], r[2048], r[16384]
     ceiling = 1.0 / (f_l1 / r1 + f_l2hit / r2 + f_mall / r3)
+    guard = json.load(open(sys.argv[4])) if len(sys.argv) > 4 else {}
     print(json.dumps({
         "workload": c["workload"],
+        **{k: guard[k] for k in ("tree_hash", "trace_vgprs") if k in guard},
         "lane_loads_per_launch": lane_loads,
         "fraction_l1": f_l1, "fraction_l2_hit": f_l2hit, "fraction_l2_miss": f_mall,
         "rate_l1_lane_loads_per_s": r1, "rate_l2_lane_loads_per_s": r2, "rate_mall_lane_loads_per_s": r3,
