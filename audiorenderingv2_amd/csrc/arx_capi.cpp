@@ -15,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -565,7 +567,28 @@ void finish_scene_image(SceneImage& img) {
 }
 }  // namespace
 
+namespace {
+// Process-wide cache of built scenes, keyed by a 128-bit hash of the input arrays: renderers and
+// groups given the same geometry (a second group for frames in flight, a C++ shim beside a Python
+// renderer) share one build.  Weak references: a scene no renderer holds any more is rebuilt.
+std::mutex g_scene_cache_mu;
+std::map<std::pair<uint64_t, uint64_t>, std::weak_ptr<const SceneImage>> g_scene_cache;
+}  // namespace
+
 SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_t n) {
+    const size_t bytes = (size_t)(n > 0 ? n : 0);
+    const std::pair<uint64_t, uint64_t> key{
+        hash_words(tri_abs, bytes * sizeof(float), hash_words(tri_v, 9 * bytes * sizeof(float), 0x9E3779B97F4A7C15ull)),
+        hash_words(tri_v, 9 * bytes * sizeof(float), hash_words(tri_abs, bytes * sizeof(float), 0x6A09E667F3BCC909ull) ^
+                                                         (uint64_t)n)};
+    {
+        std::lock_guard<std::mutex> lock(g_scene_cache_mu);
+        auto it = g_scene_cache.find(key);
+        if (it != g_scene_cache.end()) {
+            if (SceneRef hit = it->second.lock()) return hit;
+            g_scene_cache.erase(it);
+        }
+    }
     auto img = std::make_shared<SceneImage>();
     build_bvh(tri_v, tri_abs, 0.5f, n, 0, img->bvh);
     bfs_prefix_order(img->bvh, 1023);  // the top levels of the scene tree breadth-first (node locality)
@@ -574,6 +597,8 @@ SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_
     img->n_input = n;
     img->hash = scene_hash(img->bvh);
     g_scene_builds.fetch_add(1);
+    std::lock_guard<std::mutex> lock(g_scene_cache_mu);
+    g_scene_cache[key] = img;
     return img;
 }
 

@@ -100,29 +100,36 @@ def uid_path(env: dict) -> str:
     return os.path.join(tempfile.gettempdir(), "arx_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16] + ".bin")
 
 
-def share_unique_id(rank: int, world: int, env: dict, make_uid, timeout_s: float = 300.0) -> bytes | None:
-    """Rank 0's RCCL unique id to every rank (a one-rank group needs none)."""
+def share_unique_ids(rank: int, world: int, env: dict, make_uid, count: int = 1,
+                     timeout_s: float = 300.0) -> list:
+    """Rank 0's `count` RCCL unique ids (one per group: the headline group and the second group of
+    the frames-in-flight leg) to every rank; a one-rank group needs none."""
     if world == 1:
-        return None
+        return [None] * count
     path = uid_path(env)
     if rank == 0:
-        uid = make_uid()
+        ids = [make_uid() for _ in range(count)]
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "wb") as fh:
-            fh.write(uid)
+            fh.write(b"".join(ids))
         os.replace(tmp, path)
-        return uid
+        return ids
     t0 = time.monotonic()
     while time.monotonic() - t0 < timeout_s:
         try:
             with open(path, "rb") as fh:
-                uid = fh.read()
-            if len(uid) == 128:
-                return uid
+                blob = fh.read()
+            if len(blob) == 128 * count:
+                return [blob[128 * i:128 * (i + 1)] for i in range(count)]
         except FileNotFoundError:
             pass
         time.sleep(0.05)
     raise SystemExit(f"rank {rank}: no RCCL unique id from rank 0 at {path} after {timeout_s:.0f} s")
+
+
+def share_unique_id(rank: int, world: int, env: dict, make_uid, timeout_s: float = 300.0) -> bytes | None:
+    """Rank 0's RCCL unique id to every rank (a one-rank group needs none)."""
+    return share_unique_ids(rank, world, env, make_uid, 1, timeout_s)[0]
 
 
 class Ranks:
@@ -281,6 +288,41 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
                          "(projected 8-GPU rank; the all-reduce is not included)"}
 
 
+def pipelined_leg(groups, bufs, frames: int, steps: int, warmup: int, ranks: "Ranks", one_frame_ms: float) -> dict:
+    """Two frames in flight: a second renderer group on the same GPUs (same settings; the scene
+    tree is libarx's cached build, not a second one), each group on its own HIP streams, steps
+    alternating between them.  Step k's trace can then fill the SIMDs step k-1's persistent waves
+    leave as they finish (the launch tail), and a latency-bound launch (C2: about one ray per lane)
+    shares the GPU with the next one.  Same per-step work and results as the headline loop (the
+    IRs are compared); reported beside it, not as `value`."""
+    def step(k):
+        g = groups[k % len(groups)]
+        g.render(timed=False)
+        for m, (x, ol, orr) in zip(g.members, bufs[k % len(groups)]):
+            m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
+
+    for k in range(warmup * len(groups)):
+        step(k)
+    for g in groups:
+        g.synchronize()
+    ranks.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    for g in groups:
+        g.synchronize()
+    ranks.barrier()
+    elapsed = ranks.max(time.perf_counter() - t0)
+    q = int(round(ranks.sum(sum(int(g.stats()["queries"]) for g in groups) / len(groups))))
+    a, b = groups[0].member(0).get_ir(), groups[1].member(0).get_ir()
+    same = bool(np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32)) and
+                np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)))
+    ms = elapsed / steps * 1e3
+    return {"frames_in_flight": len(groups), "value": q * steps / elapsed, "unit": "ray-bounces/s", "steps": steps,
+            "ms_per_step": ms, "speedup_vs_one_frame": one_frame_ms / ms, "irs_identical": same,
+            "method": "two renderer groups (shared scene build), own streams, steps alternating; wall clock of K steps"}
+
+
 def streaming_leg(m, audio, block: int) -> dict:
     """C3's streaming overlap-add leg: the same audio fed through the streaming convolution
     (arx_stream_*: uniformly partitioned overlap-save, f64) in 4096-frame blocks, device-resident
@@ -364,6 +406,7 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
+    ap.add_argument("--no-pipelined", action="store_true", help="skip the two-frames-in-flight leg")
     ap.add_argument("--process-group", action="store_true",
                     help="take the one-GPU-per-process (RCCL rank) path even at one rank: a rehearsal of the "
                          "torch.distributed.run path on a one-GPU box")
@@ -403,9 +446,10 @@ def main(argv=None) -> int:
     t_setup = time.perf_counter()
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
         if plan["mode"] == "rank":
-            uid = share_unique_id(rank, world, os.environ, RenderGroup.unique_id)
-            g = RenderGroup.rank(settings, world, rank, uid, scene=scene, receiver=receiver)
+            uids = share_unique_ids(rank, world, os.environ, RenderGroup.unique_id, 2)
+            g = RenderGroup.rank(settings, world, rank, uids[0], scene=scene, receiver=receiver)
         else:
+            uids = [None, None]
             g = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
     ranks = Ranks(g, plan["mode"])
     ranks.barrier()
@@ -581,6 +625,23 @@ def main(argv=None) -> int:
             shard = total_rays // 8
             result["moving_listener_rank_of_8"] = moving_listener_rank_shape(settings, scene, receiver,
                                                                              args.c5_frames, shard)
+    if not args.no_pipelined:
+        with _stdout_to_stderr():
+            if plan["mode"] == "rank":
+                g2 = RenderGroup.rank(settings, world, rank, uids[1], scene=scene, receiver=receiver)
+            else:
+                g2 = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
+        g2.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        g2.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+        bufs2 = [(DeviceBuffer.from_numpy(m.settings.device, audio_np), DeviceBuffer(m.settings.device, 4 * frames),
+                  DeviceBuffer(m.settings.device, 4 * frames)) for m in g2.members]
+        g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)  # back to the headline pose (C5 moved it)
+        result["pipelined"] = pipelined_leg([g, g2], [bufs, bufs2], frames, args.steps, args.warmup, ranks,
+                                            elapsed / args.steps * 1e3)
+        for b in bufs2:
+            for x in b:
+                x.close()
+        g2.close()
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
         result["streaming"] = streaming_leg(m0, audio_np, 4096)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

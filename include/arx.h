@@ -105,7 +105,8 @@ arx_status arx_memcpy(int32_t device, void* dst, const void* src, size_t bytes);
  * (version)" into buf[len]. */
 arx_status arx_runtime_info(char* buf, size_t len);
 /* Scene trees built by this process so far (arx_set_scene / arx_group_set_scene): a group builds
- * its tree once and shares it between its members. */
+ * its tree once and shares it between its members, and geometry identical to a scene some renderer
+ * still holds reuses that build (a process-wide cache keyed by a 128-bit hash of the arrays). */
 uint64_t arx_scene_build_count(void);
 
 /* Static scene geometry: AudioRenderer::buildAccel + buildSBT (AudioRenderer.cpp:95-218, 413-464),

@@ -43,6 +43,9 @@ def test_bench_prints_one_contract_line():
     # libarx ran on the ROCm runtime it was built against (no other GPU framework in the process)
     assert "/opt/rocm" in d["runtime"].split("rccl=")[1], d["runtime"]
     assert d["trace_kernel_build"]["waves_per_simd"] == d["trace_kernel_build"]["waves_target"]
+    # two frames in flight: same per-step work, identical IRs
+    p = d["pipelined"]
+    assert p["frames_in_flight"] == 2 and p["irs_identical"] and p["value"] > 0
 
 
 def test_bench_refuses_more_gpus_than_the_box_has():
