@@ -515,7 +515,7 @@ def main(argv=None) -> int:
     moving = moving_listener(g, ranks, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
     bpb = bytes_per_bounce(n_tris)
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
-    traffic, traffic_why = profile_guard(load_profile("trace_traffic.json"), args.workload, st0)
+    traffic, traffic_why = profile_guard(load_profile(os.path.join("r03", "trace_traffic.json")), args.workload, st0)
     counts, counts_why = profile_guard(load_profile(os.path.join("r03", "trace_counts_c3.json")), args.workload, st0,
                                        ("workload", "tree_hash"))
     td, td_why = profile_guard(load_profile(os.path.join("r03", "trace_td_c3.json")), args.workload, st0)
@@ -568,7 +568,7 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "traffic_source": "profiles/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
+            "traffic_source": "profiles/r03/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
                               "build, tree and workload; PMC counters cannot be read inside this run): " + traffic_why,
             "algorithmic_bytes_per_bounce": bpb,
             "trace_launch_ms": trace_ms,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""profiles/trace_traffic.json from rocprofv3 PMC passes of the bench workload (tools/trace_once.py).
+"""profiles/r03/trace_traffic.json from rocprofv3 PMC passes of the bench workload (tools/trace_once.py).
 
 HBM-side bytes per trace launch = corrected FETCH_SIZE + WRITE_SIZE, following
 /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3): on gfx950 FETCH_SIZE counts
@@ -55,7 +55,7 @@ def main() -> int:
             guard = json.load(fh)
         out.update({k: guard[k] for k in ("tree_hash", "trace_vgprs") if k in guard})
     path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
-        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "trace_traffic.json")
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r03", "trace_traffic.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

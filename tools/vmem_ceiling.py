@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Vector-memory ceiling of the trace kernel, calibrated on this GPU.
 
-    python tools/vmem_ceiling.py profiles/r02/td_microbench_sizes.log profiles/r03/pmc_state_r03.txt \
+    python tools/vmem_ceiling.py profiles/r02/td_microbench_sizes.txt profiles/r03/pmc_state_r03.txt \
         profiles/r03/trace_counts_c3.json [guard.json] > profiles/r03/trace_vmem_ceiling.json
 
 guard.json (tools/trace_once.py ARX_GUARD_OUT of the PMC run) adds the tree hash and the trace
