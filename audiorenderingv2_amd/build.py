@@ -25,8 +25,8 @@ LIB = os.path.join(PKG, "libarx.so")
 ARCH = os.environ.get("ARX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["arx_trace.hip", "arx_receiver.hip", "arx_conv.hip", "arx_capi.cpp", "arx_group.cpp", "arx_bvh.cpp", "arx_io.cpp",
-           "arx_wide.cpp"]
-HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp", "arx_wide.hpp"]
+           "arx_wide.cpp", "arx_c2.cpp"]
+HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp", "arx_wide.hpp", "arx_c2.hpp"]
 
 COMMON = [
     "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
@@ -46,23 +46,25 @@ def _newest(paths: list[str]) -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = ()) -> str:
+def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = (), flags: tuple[str, ...] = ()) -> str:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "arx.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
     lang = ["-x", "hip"]  # host-only TUs too: they use the HIP runtime headers
-    cmd = [hipcc(), *lang, *COMMON, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
+    cmd = [hipcc(), *lang, *COMMON, *[f"-D{d}" for d in defines], *flags, "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
     return obj
 
 
-def build(force: bool = False, verbose: bool = False, exp: str | None = None, defines: tuple[str, ...] = ()) -> str:
+def build(force: bool = False, verbose: bool = False, exp: str | None = None, defines: tuple[str, ...] = (),
+          flags: tuple[str, ...] = ()) -> str:
     """The product libarx.so; with exp="<tag>", a design-experiment library
     tools/experiments/lib/libarx_<tag>.so built with the given -D macros (ARX_TRACE_*,
-    ARX_LDS_STACK), loaded by tools through ARX_LIB.  The product build takes no macros."""
+    ARX_LDS_STACK) and extra compiler flags, loaded by tools through ARX_LIB.  The product build
+    takes neither."""
     objdir, lib = OBJDIR, LIB
     if exp:
         objdir = os.path.join(REPO, "tools", "experiments", "obj", exp)
@@ -75,7 +77,7 @@ def build(force: bool = False, verbose: bool = False, exp: str | None = None, de
         for f in os.listdir(objdir):
             os.remove(os.path.join(objdir, f))
     with cf.ThreadPoolExecutor(max_workers=min(4, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, objdir, tuple(defines)), srcs))
+        objs = list(ex.map(lambda s: _compile(s, objdir, tuple(defines), tuple(flags)), srcs))
     if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest(objs):
         return lib
     # RCCL for the multi-GPU groups' IR all-reduce (arx_group.cpp), from the ROCm install
@@ -96,10 +98,11 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--exp", help="design-experiment library tag (tools/experiments/lib/libarx_<tag>.so)")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="macro for --exp builds")
+    ap.add_argument("--flag", dest="flags", action="append", default=[], help="compiler flag for --exp builds")
     args = ap.parse_args(argv)
-    if args.defines and not args.exp:
-        ap.error("-D is only for --exp builds")
-    build(force=args.force, verbose=True, exp=args.exp, defines=tuple(args.defines))
+    if (args.defines or args.flags) and not args.exp:
+        ap.error("-D / --flag are only for --exp builds")
+    build(force=args.force, verbose=True, exp=args.exp, defines=tuple(args.defines), flags=tuple(args.flags))
     return 0
 
 

@@ -31,6 +31,9 @@
 #ifndef ARX_TRACE_PKFMA
 #define ARX_TRACE_PKFMA 0  // 1: packed fma for each slab's plane pair (design experiment)
 #endif
+#ifndef ARX_TRACE_KEEPHIT
+#define ARX_TRACE_KEEPHIT 1  // the closest hit's V, W, det kept from the leaf test for shading (0: re-test)
+#endif
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
 #endif
@@ -38,7 +41,20 @@
 namespace arx {
 namespace {
 
-constexpr int kBlock = 128;
+#ifndef ARX_TRACE_BLOCK
+#define ARX_TRACE_BLOCK 128
+#endif
+#ifndef ARX_TRACE_NCACHE
+#define ARX_TRACE_NCACHE 0
+#endif
+constexpr int kBlock = ARX_TRACE_BLOCK;
+// Top-of-tree node cache: the 16-bit path copies quantized nodes [0, kNodeCache) (the top node, then
+// the scene tree's breadth-first prefix, bfs_prefix_order) into LDS at launch and reads them from
+// there.  Those nodes take a large share of the node steps (arx_debug_wide_stats [16..31]) and
+// would otherwise be L1 hits that still cost the TD its per-lane cycles.  The node buffer always
+// holds >= 1025 nodes (ensure_device_scene allocates n_nodes + 1024), so the copy stays in bounds.
+constexpr int kNodeCache = ARX_TRACE_NCACHE;
+static_assert(kNodeCache >= 0 && kNodeCache <= 1024, "node cache: at most the buffer's 1024 spare nodes");
 
 // ------------------------------------------------------------------- RNG ---
 __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
@@ -222,18 +238,33 @@ __device__ __forceinline__ bool tri_test(const Ray& r, float4 p0, float4 p1, flo
 
 // Triangles [unit, unit + 3*count) of a 16-B-unit array (TriRec = 3 units): d_tris for the BVH2
 // trees, the CW4 buffer's leaf blocks for CW4.  best = the closest hit's unit.
-__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count,
-                                          float& best_t, int& best_id, int& best) {
+// The closest hit so far of one query: t, triangle id (tie-break), the TriRec's unit (-1 none) and,
+// with ARX_TRACE_KEEPHIT, the test's V, W and det, so shade() needs no second triangle test.
+struct Best {
+    float t;
+    int id;
+    int unit;
+#if ARX_TRACE_KEEPHIT
+    float v, w, det;
+#endif
+};
+
+__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count, Best& b) {
     for (int k = 0; k < count; ++k) {
         const float4* tp = base + unit + 3 * k;
         const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
         Hit h;
         if (tri_test(r, p0, p1, p2, h)) {
             const int id = __float_as_int(p1.w);
-            if (h.t < best_t || (h.t == best_t && id < best_id)) {
-                best_t = h.t;
-                best_id = id;
-                best = unit + 3 * k;
+            if (h.t < b.t || (h.t == b.t && id < b.id)) {
+                b.t = h.t;
+                b.id = id;
+                b.unit = unit + 3 * k;
+#if ARX_TRACE_KEEPHIT
+                b.v = h.V;
+                b.w = h.W;
+                b.det = h.det;
+#endif
             }
         }
     }
@@ -275,7 +306,8 @@ __device__ __forceinline__ void ray_init(const TraceArgs& a, RayState& s, uint64
 // __closesthit__radiance (devicePrograms.cu:62-180) for TriRec `hit`, or __miss__radiance
 // (:186-190) when hit < 0.  r is the ray the query was traced with.
 __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restrict__ tbase, RayState& s, const Ray& r,
-                                      int hit, uint32_t& n_rx, uint32_t& n_miss) {
+                                      const Best& best, uint32_t& n_rx, uint32_t& n_miss) {
+    const int hit = best.unit;
     if (hit < 0) {
         ++n_miss;
         s.depth = -1;
@@ -291,10 +323,15 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
     const float3 U = sub3(P2, P1), V = sub3(P3, P1);
     const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
     const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
+#if ARX_TRACE_KEEPHIT  // the leaf test's values for this triangle and ray (the same arithmetic)
+    const float bu = best.v / best.det;
+    const float bv = best.w / best.det;
+#else
     Hit h;
     tri_test(r, p0, p1, p2, h);
     const float bu = h.V / h.det;
     const float bv = h.W / h.det;
+#endif
     const float w0 = (1.0f - bu) - bv;
     const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
     const float3 seg = sub3(P, s.pos);
@@ -365,9 +402,7 @@ __device__ __forceinline__ void flush_counters(const TraceArgs& a, uint32_t n_q,
 // node: the lane's next stack entry -- >= 0 an inner node, <= -2 a pending leaf
 // ~(first*16 + count), -1 done.  Empty children carry a 0-triangle leaf code (kEmptyChildCode).
 struct Trav {
-    float best_t;
-    int best_id;
-    int best;  // TriRec index of the closest hit so far, -1 = none
+    Best best;  // closest hit so far
     int node;
     int sp;    // stack depth
 };
@@ -409,7 +444,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p) {
 //   f32: the coded BvhNode (56 of its 64 B), ix = inv, oix = o*inv.
 template <int FMT, typename Stack>
 __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
-                                          __amdgpu_buffer_rsrc_t rs) {
+                                          __amdgpu_buffer_rsrc_t rs, const uint4* __restrict__ ncache) {
     constexpr bool Q16 = FMT == kFmtQ16;
     // the pop candidate is read first, so its latency hides under the node fetch (slot sp - 1 is
     // not touched by this step's write to slot sp)
@@ -421,9 +456,26 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     int c0, c1;
     uint4 A = make_uint4(0u, 0u, 0u, 0u), B = A;
     if constexpr (Q16) {
-        const int off = t.node * (int)sizeof(QNode2);
-        A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        if constexpr (kNodeCache > 0) {
+            // every lane reads the LDS copy (clamped index; a few cycles per wave) and only the
+            // lanes below the cached prefix skip the global fetch: separate registers for the two,
+            // so the LDS reads never wait behind the buffer loads
+            const bool cached = t.node < kNodeCache;
+            uint4 Ag = make_uint4(0u, 0u, 0u, 0u), Bg = Ag;
+            if (!cached) {
+                const int off = t.node * (int)sizeof(QNode2);
+                Ag = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+                Bg = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+            }
+            const int ci = 2 * min(t.node, kNodeCache - 1);
+            const uint4 Al = ncache[ci], Bl = ncache[ci + 1];
+            A = make_uint4(cached ? Al.x : Ag.x, cached ? Al.y : Ag.y, cached ? Al.z : Ag.z, cached ? Al.w : Ag.w);
+            B = make_uint4(cached ? Bl.x : Bg.x, cached ? Bl.y : Bg.y, cached ? Bl.z : Bg.z, cached ? Bl.w : Bg.w);
+        } else {
+            const int off = t.node * (int)sizeof(QNode2);
+            A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+            B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+        }
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
         nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
         nc = make_float4((float)(A.z & 0xffffu), (float)(A.z >> 16), (float)(B.z & 0xffffu), (float)(B.z >> 16));
@@ -466,9 +518,9 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
         const float nz1 = __builtin_fmaf((float)(bzw & 0xffffu), iz, -oiz), fz1 = __builtin_fmaf((float)(bzw >> 16), iz, -oiz);
 #endif
         tn0 = fmaxf(fmaxf(fmaxf(nx0, ny0), nz0), 0.0f);
-        tf0 = fminf(fminf(fminf(fx0, fy0), fz0), t.best_t);
+        tf0 = fminf(fminf(fminf(fx0, fy0), fz0), t.best.t);
         tn1 = fmaxf(fmaxf(fmaxf(nx1, ny1), nz1), 0.0f);
-        tf1 = fminf(fminf(fminf(fx1, fy1), fz1), t.best_t);
+        tf1 = fminf(fminf(fminf(fx1, fy1), fz1), t.best.t);
     } else {
         const float x00 = __builtin_fmaf(na.x, ix, -oix), x01 = __builtin_fmaf(na.y, ix, -oix);
         const float y00 = __builtin_fmaf(na.z, iy, -oiy), y01 = __builtin_fmaf(na.w, iy, -oiy);
@@ -477,9 +529,9 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
         const float y10 = __builtin_fmaf(nb.z, iy, -oiy), y11 = __builtin_fmaf(nb.w, iy, -oiy);
         const float z10 = __builtin_fmaf(nc.z, iz, -oiz), z11 = __builtin_fmaf(nc.w, iz, -oiz);
         tn0 = fmaxf(fmaxf(fminf(x00, x01), fminf(y00, y01)), fmaxf(fminf(z00, z01), 0.0f));
-        tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best_t));
+        tf0 = fminf(fminf(fmaxf(x00, x01), fmaxf(y00, y01)), fminf(fmaxf(z00, z01), t.best.t));
         tn1 = fmaxf(fmaxf(fminf(x10, x11), fminf(y10, y11)), fmaxf(fminf(z10, z11), 0.0f));
-        tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best_t));
+        tf1 = fminf(fminf(fmaxf(x10, x11), fmaxf(y10, y11)), fminf(fmaxf(z10, z11), t.best.t));
     }
     const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
     const bool near1 = h1 & (!h0 | (tn1 < tn0));
@@ -561,10 +613,10 @@ __device__ __forceinline__ void node_step_w4(const Ray& r, float oix, float oiy,
     const int base = (int)B.w;
     const float inf = __builtin_huge_valf();
     float tf0, tf1, tf2, tf3;
-    const float tn0 = w4_child<0>(w, sx, bx, sy, by, sz, bz, t.best_t, tf0);
-    const float tn1 = w4_child<1>(w, sx, bx, sy, by, sz, bz, t.best_t, tf1);
-    const float tn2 = w4_child<2>(w, sx, bx, sy, by, sz, bz, t.best_t, tf2);
-    const float tn3 = w4_child<3>(w, sx, bx, sy, by, sz, bz, t.best_t, tf3);
+    const float tn0 = w4_child<0>(w, sx, bx, sy, by, sz, bz, t.best.t, tf0);
+    const float tn1 = w4_child<1>(w, sx, bx, sy, by, sz, bz, t.best.t, tf1);
+    const float tn2 = w4_child<2>(w, sx, bx, sy, by, sz, bz, t.best.t, tf2);
+    const float tn3 = w4_child<3>(w, sx, bx, sy, by, sz, bz, t.best.t, tf3);
     const uint32_t m0 = meta & 3u, m1 = (meta >> 2) & 3u, m2 = (meta >> 4) & 3u, m3 = (meta >> 6) & 3u;
     float k0 = ((tn0 <= tf0) & (m0 != 0u)) ? tn0 : inf;
     float k1 = ((tn1 <= tf1) & (m1 != 0u)) ? tn1 : inf;
@@ -600,8 +652,8 @@ __device__ __forceinline__ void node_step_w4(const Ray& r, float oix, float oiy,
 template <int FMT, typename Stack>
 __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, const Ray& r, Trav& t, const Stack& stk) {
     const int v = ~t.node;
-    if constexpr (FMT == kFmtW4) leaf_hits(tbase, r, v >> 2, v & 3, t.best_t, t.best_id, t.best);
-    else leaf_hits(tbase, r, 3 * (v >> 4), v & 15, t.best_t, t.best_id, t.best);
+    if constexpr (FMT == kFmtW4) leaf_hits(tbase, r, v >> 2, v & 3, t.best);
+    else leaf_hits(tbase, r, 3 * (v >> 4), v & 15, t.best);
     const int sp = t.sp;
     const int sp_pop = max(sp - 1, 0);
     int top = stk.read(sp_pop);
@@ -659,6 +711,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     constexpr bool Q16 = FMT == kFmtQ16;
     constexpr bool W4 = FMT == kFmtW4;
     __shared__ int stk_lds[GSTACK ? 1 : kLdsStack * BLOCK];
+    __shared__ uint4 ncache[(Q16 && kNodeCache > 0) ? 2 * kNodeCache : 1];
+    if constexpr (Q16 && kNodeCache > 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(a.qnodes);
+        for (int i = threadIdx.x; i < 2 * kNodeCache; i += BLOCK) ncache[i] = q[i];
+        __syncthreads();
+    }
     // Hold the VGPR allocation at the count that fits exactly MINW waves per SIMD (see
     // ARX_TRACE_VGPR_FENCE): the kernel needs ~74, which would let the dispatcher put 6 waves on
     // some SIMDs and 4 on others.
@@ -715,9 +773,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     s.depth = -1;
     Ray r;
     Trav t;
-    t.best_t = __builtin_huge_valf();
-    t.best_id = 0x7fffffff;
-    t.best = -1;
+    t.best.t = __builtin_huge_valf();
+    t.best.id = 0x7fffffff;
+    t.best.unit = -1;
     t.node = -1;
     t.sp = 0;
     float oix = 0.f, oiy = 0.f, oiz = 0.f;
@@ -783,9 +841,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                 oiy = r.o[1] * r.inv[1];
                 oiz = r.o[2] * r.inv[2];
             }
-            t.best_t = __builtin_huge_valf();
-            t.best_id = 0x7fffffff;
-            t.best = -1;
+            t.best.t = __builtin_huge_valf();
+            t.best.id = 0x7fffffff;
+            t.best.unit = -1;
             t.node = 0;  // the top node (node 0; unit 0 of the CW4 buffer)
             t.sp = 0;
             trav = true;
@@ -818,7 +876,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                         ++n_steps;
 #endif
                         if constexpr (W4) node_step_w4(r, oix, oiy, oiz, t, stk, nrs);
-                        else node_step<FMT>(r, oix, oiy, oiz, t, stk, nrs);
+                        else node_step<FMT>(r, oix, oiy, oiz, t, stk, nrs, ncache);
                     }
                 }
             } else {
@@ -917,32 +975,51 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
 #ifndef ARX_TRACE_LEAF_THRESH
 #define ARX_TRACE_LEAF_THRESH 12
 #endif
+#ifndef ARX_TRACE_SMALL_BLOCK
+#define ARX_TRACE_SMALL_BLOCK 256  // block size of launches without the ray pool (0: kBlock)
+#endif
+constexpr int kSmallBlock = ARX_TRACE_SMALL_BLOCK;
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
 constexpr int kSimdsPerCu = 4;
 
+// Persistent grid of BLOCK-lane blocks: exactly kWaves waves per SIMD on every CU, fewer blocks
+// for small launches (one ray per lane).
+template <int BLOCK, bool GSTACK, int FMT>
+int trace_grid(const TraceArgs& args, int cus, uint64_t n_rays) {
+    constexpr int per_cu = kSimdsPerCu * kWaves * 64 / BLOCK;
+    static_assert(per_cu * BLOCK == kSimdsPerCu * kWaves * 64, "blocks must fill the CU's wave slots exactly");
+    const uint64_t want = (n_rays + BLOCK - 1) / BLOCK;
+    uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
+    if (GSTACK || FMT == kFmtW4) cap = std::min<uint64_t>(cap, args.gstack_lanes / BLOCK);  // one stack column per lane
+    return (int)std::max<uint64_t>(1, std::min(want, cap));
+}
+
 template <int FMT, bool GSTACK>
 hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
-    auto k = trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>;
     const uint64_t n_rays = args.ray_end - args.ray_begin;
-    // persistent grid: exactly kWaves waves per SIMD on every CU, fewer blocks for small launches
-    // (one ray per lane)
-    constexpr int per_cu = kSimdsPerCu * kWaves * 64 / kBlock;
 #ifdef ARX_TRACE_DYN_LDS
     static const size_t dyn_lds = ARX_TRACE_DYN_LDS;  // design experiments only
 #else
     static const size_t dyn_lds = 0;
 #endif
-    const uint64_t want = (n_rays + kBlock - 1) / kBlock;
-    uint64_t cap = (uint64_t)per_cu * (uint64_t)(cus > 0 ? cus : 256);
-    if (GSTACK || FMT == kFmtW4) cap = std::min<uint64_t>(cap, args.gstack_lanes / kBlock);  // one stack column per lane
-    const int grid = (int)std::max<uint64_t>(1, std::min(want, cap));
+    const int grid = trace_grid<kBlock, GSTACK, FMT>(args, cus, n_rays);
     TraceArgs a2 = args;
     const bool dyn = n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
     a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
     a2.dyn_chunk = (uint32_t)kDynChunk;
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), dyn_lds, s, a2);
+    if (kSmallBlock > 0 && !dyn) {
+        // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
+        // one wave per SIMD each: 0.465 -> 0.44 ms at C2
+        constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
+        const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, n_rays);
+        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(g2), dim3(SB),
+                           dyn_lds, s, a2);
+    } else {
+        hipLaunchKernelGGL((trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(grid),
+                           dim3(kBlock), dyn_lds, s, a2);
+    }
     return hipGetLastError();
 }
 

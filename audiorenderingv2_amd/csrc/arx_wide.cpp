@@ -7,6 +7,7 @@
 #include "arx_wide.hpp"
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -275,6 +276,7 @@ extern "C" arx_status arx_debug_wide_stats(const float* tri_v, const float* tri_
     uint64_t queries = 0, q2_steps = 0, q2_tris = 0, q4_steps = 0, q4_tris = 0, mism = 0, misses = 0;
     int max_stack = 0;
     std::vector<uint64_t> stack_hist(64, 0);
+    std::vector<uint64_t> visits(q2.size() + 2, 0);  // BVH2 node steps per node
     for (int64_t ray = 0; ray < n_rays; ++ray) {
         const double cz = 2.0 * U(rng) - 1.0, ph = 2.0 * M_PI * U(rng), sz = std::sqrt(std::max(0.0, 1.0 - cz * cz));
         double o[3] = {emitter[0], emitter[1], emitter[2]}, d[3] = {sz * std::cos(ph), sz * std::sin(ph), cz};
@@ -296,6 +298,7 @@ extern "C" arx_status arx_debug_wide_stats(const float* tri_v, const float* tri_
                     }
                 while (node >= 0) {
                     ++q2_steps;
+                    ++visits[(size_t)node];
                     const QNode2& qn = q2[(size_t)node - 1];
                     double tn[2];
                     int code[2];
@@ -458,5 +461,31 @@ extern "C" arx_status arx_debug_wide_stats(const float* tri_v, const float* tri_
         }
     }
     out[14] = (double)w.unit_end;
+    if (n_out >= 32) {  // share of BVH2 node steps on K = 32 .. 4096 nodes: the K most visited
+        // ([16..23]) and the K with the largest box surface area ([24..31], ray-independent)
+        std::vector<uint64_t> sorted(visits);
+        std::sort(sorted.begin(), sorted.end(), std::greater<uint64_t>());
+        std::vector<std::pair<double, int32_t>> area;
+        for (size_t i = 0; i < q2.size(); ++i)
+            for (int c = 0; c < 2; ++c) {
+                const int32_t code = q2[i].c[c].code;
+                if (code <= 0) continue;
+                double l[3], hh[3];
+                grid_box(g, q2[i].c[c].q, l, hh);
+                const double e0 = hh[0] - l[0], e1 = hh[1] - l[1], e2 = hh[2] - l[2];
+                area.push_back({-(e0 * e1 + e1 * e2 + e2 * e0), code});
+            }
+        area.push_back({-HUGE_VAL, 1});
+        std::sort(area.begin(), area.end());
+        const double steps = (double)std::max<uint64_t>(q2_steps, 1);
+        for (int j = 0; j < 8; ++j) {
+            const size_t k = (size_t)32 << j;
+            uint64_t in_top = 0, in_area = 0;
+            for (size_t i = 0; i < std::min(k, sorted.size()); ++i) in_top += sorted[i];
+            for (size_t i = 0; i < std::min(k, area.size()); ++i) in_area += visits[(size_t)area[i].second];
+            out[16 + j] = (double)in_top / steps;
+            out[24 + j] = (double)in_area / steps;
+        }
+    }
     return ARX_OK;
 }
