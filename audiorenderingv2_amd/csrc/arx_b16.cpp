@@ -1,6 +1,6 @@
-// arx_c2.cpp -- layout of the compact binary tree (C2, arx_c2.hpp) and a host simulation of its
-// traversal beside the 16-bit BVH2's (arx_debug_c2_stats).
-#include "arx_c2.hpp"
+// arx_b16.cpp -- layout of the compact binary tree (B16, arx_b16.hpp) and a host simulation of its
+// traversal beside the 16-bit BVH2's (arx_debug_b16_stats).
+#include "arx_b16.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -14,9 +14,9 @@
 
 namespace arx {
 
-bool layout_c2(const BvhNode* coded, int32_t node_base, int32_t root_node, uint32_t root_unit, uint32_t fill,
-               uint32_t first_block, C2Build& out, const char** why, int block_bits) {
-    out = C2Build();
+bool layout_b16(const BvhNode* coded, int32_t node_base, int32_t root_node, uint32_t root_unit, uint32_t fill,
+               uint32_t first_block, B16Build& out, const char** why, int block_bits) {
+    out = B16Build();
     const uint32_t bsize = 1u << block_bits;
     std::unordered_map<uint32_t, uint32_t> fill_of;  // block -> next free unit
     if (fill != 0u) fill_of[root_unit >> block_bits] = fill;
@@ -41,12 +41,12 @@ bool layout_c2(const BvhNode* coded, int32_t node_base, int32_t root_node, uint3
             const int32_t code = bn.d[c];
             kind[c] = 0u;
             if (code >= 0) {
-                kind[c] = kC2Inner;
+                kind[c] = kB16Inner;
                 ++n_inner;
             } else if (code != kEmptyChildCode) {
                 const int32_t v = ~code;
                 const uint32_t cnt = (uint32_t)(v & 15);
-                if (cnt >= kC2Inner) {
+                if (cnt >= kB16Inner) {
                     *why = "leaf of more than 14 triangles";
                     return false;
                 }
@@ -79,7 +79,7 @@ bool layout_c2(const BvhNode* coded, int32_t node_base, int32_t root_node, uint3
             }
         }
         if (base >= (1u << 24) || next_block >= ((1u << 24) >> block_bits)) {
-            *why = "C2 buffer beyond the 24-bit base";
+            *why = "B16 buffer beyond the 24-bit base";
             return false;
         }
         out.node_units.push_back(unit);
@@ -87,9 +87,9 @@ bool layout_c2(const BvhNode* coded, int32_t node_base, int32_t root_node, uint3
         out.node_w3.push_back(kind[0] | (kind[1] << 4) | (base << 8));
         uint32_t k = 0, t_units = 0;
         for (int c = 0; c < 2; ++c)
-            if (kind[c] == kC2Inner) queue.emplace_back(bn.d[c], base + k++);
+            if (kind[c] == kB16Inner) queue.emplace_back(bn.d[c], base + k++);
         for (int c = 0; c < 2; ++c)
-            if (kind[c] != kC2Inner && kind[c] != 0u)
+            if (kind[c] != kB16Inner && kind[c] != 0u)
                 for (uint32_t t = 0; t < kind[c]; ++t) {
                     out.tri_units.emplace_back(base + n_inner + t_units, first[c] + (int32_t)t);
                     t_units += (uint32_t)kTriUnits;
@@ -101,7 +101,7 @@ bool layout_c2(const BvhNode* coded, int32_t node_base, int32_t root_node, uint3
 
 }  // namespace arx
 
-// ---- host simulation (arx_debug_c2_stats) ------------------------------------------------------
+// ---- host simulation (arx_debug_b16_stats) ------------------------------------------------------
 namespace arx {
 namespace {
 
@@ -185,10 +185,10 @@ void traverse(const SRay& r, int32_t root, Hit& h, uint64_t& steps, Node node_fn
 
 using namespace arx;
 
-/* out: [0] queries [1] / [2] BVH2 node steps / triangle tests per query [3] / [4] the same for C2
- * [5] C2 frame switches per query (node steps into another block than the lane's last) [6] queries
- * whose closest hits differ [7] C2 units [8] C2 blocks [9] BVH2 nodes [10] C2 layout ok. */
-extern "C" arx_status arx_debug_c2_stats(const float* tri_v, const float* tri_abs, int64_t n, const float* emitter,
+/* out: [0] queries [1] / [2] BVH2 node steps / triangle tests per query [3] / [4] the same for B16
+ * [5] B16 frame switches per query (node steps into another block than the lane's last) [6] queries
+ * whose closest hits differ [7] B16 units [8] B16 blocks [9] BVH2 nodes [10] B16 layout ok. */
+extern "C" arx_status arx_debug_b16_stats(const float* tri_v, const float* tri_abs, int64_t n, const float* emitter,
                                          int64_t n_rays, int32_t bounces, uint64_t seed, int32_t block_bits,
                                          double* out, size_t n_out) {
     if (!emitter || !out || n_out < 11 || n_rays < 0 || bounces < 1 || block_bits < 3 || block_bits > 12)
@@ -209,14 +209,14 @@ extern "C" arx_status arx_debug_c2_stats(const float* tri_v, const float* tri_ab
     std::vector<QNode2> q2(img->coded.size() + 1);
     if (!quantize_nodes16(img->coded.data(), img->coded.size(), g, q2.data() + 1))
         return fail(ARX_ERR_INTERNAL, "grid");
-    C2Build L;
+    B16Build L;
     const char* why = "";
-    if (!layout_c2(img->coded.data(), 1, 1, kC2SceneRoot, 3, 1, L, &why, block_bits)) {
+    if (!layout_b16(img->coded.data(), 1, 1, kB16SceneRoot, 3, 1, L, &why, block_bits)) {
         out[10] = 0.0;
         return ARX_OK;
     }
     const uint32_t n_blocks = L.unit_end >> block_bits;
-    std::vector<C2FrameAcc> acc(n_blocks);
+    std::vector<B16FrameAcc> acc(n_blocks);
     for (size_t i = 0; i < L.node_units.size(); ++i)
         acc[L.node_units[i] >> block_bits].add(q2[(size_t)L.node_src[i]], L.node_w3[i]);
     std::vector<uint2> frames(n_blocks);
@@ -224,7 +224,7 @@ extern "C" arx_status arx_debug_c2_stats(const float* tri_v, const float* tri_ab
     std::vector<uint4> units(L.unit_end, make_uint4(0u, 0u, 0u, 0u));
     for (size_t i = 0; i < L.node_units.size(); ++i)
         units[L.node_units[i]] =
-            c2_node(q2[(size_t)L.node_src[i]], L.node_w3[i], frames[L.node_units[i] >> block_bits]);
+            b16_node(q2[(size_t)L.node_src[i]], L.node_w3[i], frames[L.node_units[i] >> block_bits]);
     std::vector<int32_t> unit_tri(L.unit_end, -1);
     for (const auto& ut : L.tri_units) unit_tri[ut.first] = ut.second;
 
@@ -267,7 +267,7 @@ extern "C" arx_status arx_debug_c2_stats(const float* tri_v, const float* tri_ab
                     }
                 });
             traverse(
-                r, (int32_t)kC2SceneRoot, hc, sc,
+                r, (int32_t)kB16SceneRoot, hc, sc,
                 [&](int32_t u, double lo2[2][3], double hi2[2][3], int32_t code[2]) {
                     const uint32_t blk = (uint32_t)u >> block_bits;
                     if (blk != cur_block) {
@@ -286,7 +286,7 @@ extern "C" arx_status arx_debug_c2_stats(const float* tri_v, const float* tri_ab
                             hi2[c][k] = (double)g.origin[k] + (double)(of[k] + (qh << e[k])) * (double)g.scale[k];
                         }
                     const uint32_t k0 = w.w & 15u, k1 = (w.w >> 4) & 15u, base = w.w >> 8;
-                    const uint32_t i0 = k0 == kC2Inner, i1 = k1 == kC2Inner, n_in = i0 + i1;
+                    const uint32_t i0 = k0 == kB16Inner, i1 = k1 == kB16Inner, n_in = i0 + i1;
                     code[0] = i0 ? (int32_t)base : ~(int32_t)((base + n_in) * 16u + k0);
                     code[1] = i1 ? (int32_t)(base + i0) : ~(int32_t)((base + n_in + 3u * (i0 ? 0u : k0)) * 16u + k1);
                 },

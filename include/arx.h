@@ -309,12 +309,12 @@ arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, si
 arx_status arx_debug_wide_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
                                 const float* emitter, int64_t n_rays, int32_t bounces, uint64_t seed, double* out,
                                 size_t n_out);
-/* Host only: the scene's 16-bit BVH2 and its compact copy (C2: one 16-B unit per node, 8-bit planes
+/* Host only: the scene's 16-bit BVH2 and its compact copy (B16: one 16-B unit per node, 8-bit planes
  * on frames shared by blocks of 2^block_bits units) traversed on the CPU in the trace kernel's order
  * over the same bouncing rays; out[11]: [0] queries, [1] / [2] BVH2 node steps / triangle tests per
- * query, [3] / [4] the same for C2, [5] C2 frame switches per query, [6] queries whose closest hits
- * differ, [7] C2 units, [8] C2 blocks, [9] BVH2 nodes, [10] 1 if the layout succeeded. */
-arx_status arx_debug_c2_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
+ * query, [3] / [4] the same for B16, [5] B16 frame switches per query, [6] queries whose closest hits
+ * differ, [7] B16 units, [8] B16 blocks, [9] BVH2 nodes, [10] 1 if the layout succeeded. */
+arx_status arx_debug_b16_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
                               const float* emitter, int64_t n_rays, int32_t bounces, uint64_t seed,
                               int32_t block_bits, double* out, size_t n_out);
 /* Profiling builds only (ARX_TRACE_PROF=1, tools/trace_profile.py): the last trace launch's
