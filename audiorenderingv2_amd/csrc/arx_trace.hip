@@ -411,20 +411,28 @@ struct Trav {
 // deeper than the LDS rows): a column of bvh_depth + 1 entries at gstack[slot * lanes + gid],
 // coalesced across the wave like the LDS rows.  A stack holds at most one entry per tree level,
 // so rows > bvh_depth never overflows.
+// Both give the step two accessors: below(sp) reads the entry a pop would take (slot sp - 1; any
+// value when sp == 0) and put(sp, v) writes slot sp, the one above the top.
+//   LdsStack: slot s lives in row s + 1 and row 0 is a dummy, so below(sp) is row sp and put(sp) is
+//   row sp + 1: one address for both (the write's +1 row is the instruction's offset), no clamps --
+//   the launcher takes this stack only for trees with bvh_depth + 1 <= ROWS, and a stack holds at
+//   most one entry per level.
+//   kSentinel: below(0) is -1 (LdsStack's dummy row, written once per launch), so a pop needs no
+//   empty-stack test.
 template <int BLOCK, int ROWS>
 struct LdsStack {
+    static constexpr bool kSentinel = true;
     int* base;  // &stk[lane]
-    __device__ __forceinline__ int& at(int slot) const { return base[slot * BLOCK]; }
-    __device__ __forceinline__ int read(int slot) const { return base[slot * BLOCK]; }
-    __device__ __forceinline__ int rows() const { return ROWS; }
+    __device__ __forceinline__ int below(int sp) const { return base[sp * BLOCK]; }
+    __device__ __forceinline__ void put(int sp, int v) const { base[(sp + 1) * BLOCK] = v; }
 };
 struct GlobalStack {
+    static constexpr bool kSentinel = false;
     int* base;  // &gstack[gid]
     uint64_t stride;
     int nrows;
-    __device__ __forceinline__ int& at(int slot) const { return base[(uint64_t)slot * stride]; }
-    __device__ __forceinline__ int read(int slot) const { return base[(uint64_t)slot * stride]; }
-    __device__ __forceinline__ int rows() const { return nrows; }
+    __device__ __forceinline__ int below(int sp) const { return base[(uint64_t)max(sp - 1, 0) * stride]; }
+    __device__ __forceinline__ void put(int sp, int v) const { base[(uint64_t)min(sp, nrows - 1) * stride] = v; }
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p) {
@@ -450,7 +458,7 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     // not touched by this step's write to slot sp)
     const int sp = t.sp;
     const int sp_pop = max(sp - 1, 0);
-    int top = stk.at(sp_pop);
+    int top = stk.below(sp);
     const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
     float4 na, nb, nc;
     int c0, c1;
@@ -537,14 +545,16 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     const bool near1 = h1 & (!h0 | (tn1 < tn0));
     const int c_near = near1 ? c1 : c0;
     const int c_far = near1 ? c0 : c1;
-    // The clamp only keeps the write inside the array: the stack holds at most one entry per
-    // level and rows > bvh_depth (launch_trace).
-    stk.at(min(sp, stk.rows() - 1)) = c_far;  // above the top of the stack unless pushed
+    stk.put(sp, c_far);  // above the top of the stack unless pushed
     asm volatile("" : "+v"(top));            // the pop read stays unconditional (no branch around it)
-    const bool any = h0 | h1;
-    const int popped = sp > 0 ? top : -1;
-    t.node = any ? c_near : popped;
-    t.sp = any ? sp + (int)(h0 & h1) : sp_pop;
+    const bool any = h0 | h1, both = h0 & h1;
+    if constexpr (Stack::kSentinel) {  // row 0 holds -1: a pop of the empty stack ends the query
+        t.node = any ? c_near : top;
+        t.sp = any ? (both ? sp + 1 : sp) : sp - 1;  // -1 only once the query is done
+    } else {
+        t.node = any ? c_near : (sp > 0 ? top : -1);
+        t.sp = any ? (both ? sp + 1 : sp) : sp_pop;
+    }
 }
 
 // CW4 step (arx_layout.hpp): one 32-B node = two 16-B loads for four children.  Plane q of axis k
@@ -580,6 +590,7 @@ __device__ __forceinline__ float w4_child(const uint32_t (&w)[5], float sx, floa
 
 template <int BLOCK, int ROWS>
 struct W4Stack {
+    static constexpr bool kSentinel = false;
     int* lds;        // &stk[lane]
     int* glob;       // &gstack[gid]: rows ROWS.. (overflow)
     uint64_t stride;
@@ -590,6 +601,7 @@ struct W4Stack {
         if (slot < ROWS) lds[slot * BLOCK] = v;
         else glob[(uint64_t)(slot - ROWS) * stride] = v;
     }
+    __device__ __forceinline__ int below(int sp) const { return read(max(sp - 1, 0)); }
 };
 
 template <typename Stack>
@@ -655,11 +667,15 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
     if constexpr (FMT == kFmtW4) leaf_hits(tbase, r, v >> 2, v & 3, t.best);
     else leaf_hits(tbase, r, 3 * (v >> 4), v & 15, t.best);
     const int sp = t.sp;
-    const int sp_pop = max(sp - 1, 0);
-    int top = stk.read(sp_pop);
+    int top = stk.below(sp);
     asm volatile("" : "+v"(top));
-    t.node = sp > 0 ? top : -1;
-    t.sp = sp_pop;
+    if constexpr (Stack::kSentinel) {
+        t.node = top;
+        t.sp = sp - 1;
+    } else {
+        t.node = sp > 0 ? top : -1;
+        t.sp = max(sp - 1, 0);
+    }
 }
 
 // Highest VGPR the trace kernel claims, so that its allocation (granule 8) admits exactly
@@ -710,7 +726,7 @@ template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT,
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     constexpr bool Q16 = FMT == kFmtQ16;
     constexpr bool W4 = FMT == kFmtW4;
-    __shared__ int stk_lds[GSTACK ? 1 : kLdsStack * BLOCK];
+    __shared__ int stk_lds[GSTACK ? 1 : (kLdsStack + 1) * BLOCK];  // + LdsStack's dummy row
     __shared__ uint4 ncache[(Q16 && kNodeCache > 0) ? 2 * kNodeCache : 1];
     if constexpr (Q16 && kNodeCache > 0) {
         const uint4* q = reinterpret_cast<const uint4*>(a.qnodes);
@@ -737,6 +753,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
         stk.nrows = a.bvh_depth + 1;
     } else {
         stk.base = stk_lds + lane;
+        stk_lds[lane] = -1;  // the dummy row under the stack (LdsStack::kSentinel)
     }
     const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf) : (Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes));
     const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
