@@ -121,6 +121,8 @@ SIGNATURES = {
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
     "arx_debug_wide_stats": (C.c_int, [_F, _F, C.c_int64, _F, C.c_int64, C.c_int32, C.c_uint64, _D, C.c_size_t]),
+    "arx_debug_b16_stats": (C.c_int, [_F, _F, C.c_int64, _F, C.c_int64, C.c_int32, C.c_uint64, C.c_int32, _D,
+                                      C.c_size_t]),
     "arx_debug_trace_profile": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_debug_node_images": (C.c_int, [_P, _P, _P, C.c_size_t, _F, C.POINTER(C.c_uint64)]),
     "arx_trace_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
