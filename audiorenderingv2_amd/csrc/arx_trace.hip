@@ -549,8 +549,9 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     asm volatile("" : "+v"(top));            // the pop read stays unconditional (no branch around it)
     const bool any = h0 | h1, both = h0 & h1;
     if constexpr (Stack::kSentinel) {  // row 0 holds -1: a pop of the empty stack ends the query
-        t.node = any ? c_near : top;
-        t.sp = any ? (both ? sp + 1 : sp) : sp - 1;  // -1 only once the query is done
+        // near1 -> c1; else h0 -> c0; else neither child was hit (near1 is false only with !h1 or h0)
+        t.node = near1 ? c1 : (h0 ? c0 : top);
+        t.sp = sp + (h0 ? 0 : -1) + (int)h1;  // push, continue or pop; -1 only once the query is done
     } else {
         t.node = any ? c_near : (sp > 0 ? top : -1);
         t.sp = any ? (both ? sp + 1 : sp) : sp_pop;
