@@ -725,10 +725,8 @@ QGrid make_qgrid(const float lo[3], const float hi[3], double margin_frac) {
 }
 
 namespace {
-// Outward rounding margin in grid steps.  The kernel's f32 form fma(q, scale*inv, (origin-o)*inv)
-// is off by at most 5 * 2^-24 * extent * |inv| for origins on the grid (5 roundings, each of a
-// term bounded by the extent) = 0.02 of a step of extent/65000; 0.1 step leaves a 5x margin.
-constexpr double kQMargin = 0.1;
+// Outward rounding margin in grid steps: kQ16Margin (arx_layout.hpp, with the kernel's error bound).
+constexpr double kQMargin = kQ16Margin;
 // Outward grid index of a plane (lo: floor, hi: ceil) with the margin above; < 0 / > 65535
 // when it falls outside the grid.
 int64_t q_lo(const QGrid& g, int k, float v) {

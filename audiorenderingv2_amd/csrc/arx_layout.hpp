@@ -40,8 +40,8 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
 // 16-bit quantized binary node, 32 B (2 x 16-B loads instead of 3.5 for the f32 node): the
 // coded node (code_nodes) with both child boxes on one scene-wide 16-bit grid per axis,
-// plane = grid.origin + q * grid.scale (real arithmetic), rounded outward with a 0.1-step margin so
-// the kernel's f32 slab arithmetic stays conservative (quantize_nodes16, arx_bvh.cpp).
+// plane = grid.origin + q * grid.scale (real arithmetic), rounded outward with a kQ16Margin-step
+// margin so the kernel's f32 slab arithmetic stays conservative (quantize_nodes16, arx_bvh.cpp).
 // Each 16-B half is one child: q[0..2] = x, y, z as (lo | hi << 16), code as in code_nodes.
 struct QChild {
     uint32_t q[3];
@@ -107,6 +107,13 @@ constexpr uint32_t kB16SceneRoot = 1u, kB16RecvRoot = 2u;
 // Stack-entry / child code of an empty child in the coded and quantized nodes (code_nodes,
 // arx_bvh.hpp): a leaf of 0 triangles (-1 is kept free: it means "no entry").
 constexpr int32_t kEmptyChildCode = ~16;
+
+// Outward rounding margin of QNode2 planes, in grid steps (quantize_nodes16 and its device twins in
+// arx_receiver.hip).  The trace kernel forms a plane as the float 2^23 + q straight from its bits and
+// computes t = fma(2^23 + q, ix, -C) with C = 2^23 * ix + (o - origin) * inv rounded once: that
+// rounding is at most half an ulp of C <= 0.504 step, plus < 0.02 step for the other roundings
+// (|t| <= 2^16 steps), so 0.75 step keeps every slab conservative.  A step is 1/65000 of the grid.
+constexpr double kQ16Margin = 0.75;
 
 // The scene-wide grid of QNode2 trees.
 struct QGrid {

@@ -30,12 +30,12 @@ __device__ __forceinline__ int32_t child_code(int32_t ref, int32_t count) {
     return count < 0 ? kEmptyChildCode : count == 0 ? ref : ~(ref * 16 + count);  // code_nodes (arx_bvh.cpp)
 }
 
-// Outward 16-bit grid index of a plane with the 0.1-step margin: quantize_nodes16's arithmetic
+// Outward 16-bit grid index of a plane with the kQ16Margin margin: quantize_nodes16's arithmetic
 // (arx_bvh.cpp) bit for bit (IEEE f64 division), like the device re-quantization below.
 __device__ __forceinline__ bool quantize_axis(const QGrid& g, const double* /*inv*/, int k, float lo, float hi,
                                               uint32_t& word) {
-    const double l = floor(((double)lo - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
-    const double h = ceil(((double)hi - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
+    const double l = floor(((double)lo - (double)g.origin[k]) / (double)g.scale[k] - kQ16Margin);
+    const double h = ceil(((double)hi - (double)g.origin[k]) / (double)g.scale[k] + kQ16Margin);
     if (!(l >= 0.0) || !(h <= 65535.0)) return false;
     word = (uint32_t)l | ((uint32_t)h << 16);
     return true;
@@ -275,8 +275,8 @@ __device__ __forceinline__ bool requant_child(const QGrid& g, const float* xy, c
     for (int k = 0; k < 3; ++k) {
         uint32_t ql = 1u, qh = 0u;  // empty: the slab between planes 0 and 1 (grid corner)
         if (!empty) {
-            const double l = floor(((double)lo[k] - (double)g.origin[k]) / (double)g.scale[k] - 0.1);
-            const double h = ceil(((double)hi[k] - (double)g.origin[k]) / (double)g.scale[k] + 0.1);
+            const double l = floor(((double)lo[k] - (double)g.origin[k]) / (double)g.scale[k] - kQ16Margin);
+            const double h = ceil(((double)hi[k] - (double)g.origin[k]) / (double)g.scale[k] + kQ16Margin);
             if (!(lo[k] <= hi[k]) || !(l >= 0.0) || !(h <= 65535.0)) {
                 ok = false;
                 ql = 0u;

@@ -28,8 +28,8 @@
 #include "arx_kernels.hpp"
 #include "arx_layout.hpp"
 
-#ifndef ARX_TRACE_PKFMA
-#define ARX_TRACE_PKFMA 0  // 1: packed fma for each slab's plane pair (design experiment)
+#ifndef ARX_TRACE_BITFLOAT
+#define ARX_TRACE_BITFLOAT 1  // 16-bit planes as the float 2^23 + q built by v_perm (0: u16 -> f32 conversions)
 #endif
 #ifndef ARX_TRACE_KEEPHIT
 #define ARX_TRACE_KEEPHIT 1  // the closest hit's V, W, det kept from the leaf test for shading (0: re-test)
@@ -148,7 +148,10 @@ struct Ray {
     float inv[3];    // safe reciprocal direction (box test only)
     float sx, sy, sz;
     int kx, ky, kz;
-    uint32_t nsel[3];  // v_perm selectors per axis: near plane into the low half (ARX_TRACE_SIGNSEL)
+    uint32_t nsel[3];  // v_perm selectors per axis: the near plane (ARX_TRACE_SIGNSEL, node_step)
+#if ARX_TRACE_BITFLOAT
+    uint32_t fsel[3];  // ... and the far plane
+#endif
 };
 
 __device__ __forceinline__ float sel3(float x, float y, float z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
@@ -187,9 +190,16 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
         float v = dd[k];
         if (fabsf(v) < 1e-20f) v = (v < 0.0f) ? -1e-20f : 1e-20f;
         r.inv[k] = __builtin_amdgcn_rcpf(v);
+#if ARX_TRACE_BITFLOAT
+        // a (lo | hi << 16) plane word: near = lo for a positive reciprocal, hi for a negative one;
+        // bytes 4-5 (lo) or 6-7 (hi) of {word, 2^23} under 2^23's upper bytes 2-3
+        r.nsel[k] = r.inv[k] >= 0.0f ? 0x03020504u : 0x03020706u;
+        r.fsel[k] = r.inv[k] >= 0.0f ? 0x03020706u : 0x03020504u;
+#else
         // a (lo | hi << 16) plane word: keep for a positive reciprocal (lo is the near plane), swap
         // the halves for a negative one
         r.nsel[k] = r.inv[k] >= 0.0f ? 0x03020100u : 0x01000302u;
+#endif
     }
 }
 
@@ -504,20 +514,23 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
         // word: no min / max per slab.  The fma is monotone in q, so the near plane's t is the
         // min of the two and the result is the min / max form's, bit for bit; an empty child's
         // (1, 0) planes come out near > far on either sign.
+#if ARX_TRACE_BITFLOAT
+        // Each plane straight from its bits: v_perm puts the near (far) 16-bit half under the
+        // exponent byte of 2^23, giving the float 2^23 + q exactly, and oix here is
+        // C = fma(2^23, ix, (o - origin) * inv) (trace_kernel): t = fma(2^23 + q, ix, -C) is
+        // q * ix - (o - origin) * inv up to C's rounding, <= 0.504 step, which the kQ16Margin
+        // outward rounding of every plane covers (arx_layout.hpp).  No int -> float conversions.
+        auto pl = [](uint32_t w, uint32_t sel) { return __uint_as_float(__builtin_amdgcn_perm(w, 0x4B000000u, sel)); };
+        const float nx0 = __builtin_fmaf(pl(A.x, r.nsel[0]), ix, -oix), fx0 = __builtin_fmaf(pl(A.x, r.fsel[0]), ix, -oix);
+        const float ny0 = __builtin_fmaf(pl(A.y, r.nsel[1]), iy, -oiy), fy0 = __builtin_fmaf(pl(A.y, r.fsel[1]), iy, -oiy);
+        const float nz0 = __builtin_fmaf(pl(A.z, r.nsel[2]), iz, -oiz), fz0 = __builtin_fmaf(pl(A.z, r.fsel[2]), iz, -oiz);
+        const float nx1 = __builtin_fmaf(pl(B.x, r.nsel[0]), ix, -oix), fx1 = __builtin_fmaf(pl(B.x, r.fsel[0]), ix, -oix);
+        const float ny1 = __builtin_fmaf(pl(B.y, r.nsel[1]), iy, -oiy), fy1 = __builtin_fmaf(pl(B.y, r.fsel[1]), iy, -oiy);
+        const float nz1 = __builtin_fmaf(pl(B.z, r.nsel[2]), iz, -oiz), fz1 = __builtin_fmaf(pl(B.z, r.fsel[2]), iz, -oiz);
+#else
         const uint32_t ax = __builtin_amdgcn_perm(A.x, A.x, r.nsel[0]), ay = __builtin_amdgcn_perm(A.y, A.y, r.nsel[1]);
         const uint32_t az = __builtin_amdgcn_perm(A.z, A.z, r.nsel[2]), bxw = __builtin_amdgcn_perm(B.x, B.x, r.nsel[0]);
         const uint32_t byw = __builtin_amdgcn_perm(B.y, B.y, r.nsel[1]), bzw = __builtin_amdgcn_perm(B.z, B.z, r.nsel[2]);
-#if ARX_TRACE_PKFMA  // near and far plane of one slab in one packed fma (v_pk_fma_f32)
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        auto slab = [](uint32_t w, float i, float oi) -> f2 {
-            const f2 q = {(float)(w & 0xffffu), (float)(w >> 16)};
-            return __builtin_elementwise_fma(q, (f2){i, i}, (f2){-oi, -oi});
-        };
-        const f2 sx0 = slab(ax, ix, oix), sy0 = slab(ay, iy, oiy), sz0 = slab(az, iz, oiz);
-        const f2 sx1 = slab(bxw, ix, oix), sy1 = slab(byw, iy, oiy), sz1 = slab(bzw, iz, oiz);
-        const float nx0 = sx0.x, fx0 = sx0.y, ny0 = sy0.x, fy0 = sy0.y, nz0 = sz0.x, fz0 = sz0.y;
-        const float nx1 = sx1.x, fx1 = sx1.y, ny1 = sy1.x, fy1 = sy1.y, nz1 = sz1.x, fz1 = sz1.y;
-#else
         const float nx0 = __builtin_fmaf((float)(ax & 0xffffu), ix, -oix), fx0 = __builtin_fmaf((float)(ax >> 16), ix, -oix);
         const float ny0 = __builtin_fmaf((float)(ay & 0xffffu), iy, -oiy), fy0 = __builtin_fmaf((float)(ay >> 16), iy, -oiy);
         const float nz0 = __builtin_fmaf((float)(az & 0xffffu), iz, -oiz), fz0 = __builtin_fmaf((float)(az >> 16), iz, -oiz);
@@ -854,6 +867,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                 r.inv[0] *= a.qgrid.scale[0];
                 r.inv[1] *= a.qgrid.scale[1];
                 r.inv[2] *= a.qgrid.scale[2];
+#if ARX_TRACE_SIGNSEL && ARX_TRACE_BITFLOAT
+                if constexpr (Q16) {  // node_step's C = 2^23 * ix + (o - origin) * inv, one rounding
+                    oix = __builtin_fmaf(8388608.0f, r.inv[0], oix);
+                    oiy = __builtin_fmaf(8388608.0f, r.inv[1], oiy);
+                    oiz = __builtin_fmaf(8388608.0f, r.inv[2], oiz);
+                }
+#endif
             } else {
                 oix = r.o[0] * r.inv[0];
                 oiy = r.o[1] * r.inv[1];
