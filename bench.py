@@ -587,13 +587,18 @@ def main(argv=None) -> int:
         },
     }
     if vmem and counts:
-        # the trace's divergent 16-B gathers against their microbenchmark-calibrated ceiling for this
-        # kernel's L1 / L2 / Infinity-Cache hit mix (tools/vmem_ceiling.py)
+        # the trace's divergent 16-B gathers against the rate a microbenchmark of independent
+        # divergent gathers reaches at this kernel's L1 / L2 / Infinity-Cache hit mix
+        # (tools/vmem_ceiling.py).  A reference rate, not a hard ceiling: lanes of a wave share the
+        # top nodes and a node's two 16-B halves share one 64-B block, which the microbenchmark's
+        # one-block-per-lane pattern does not model, so frac may pass 1.
         lane_rate = counts["lane_loads_16B_per_query"] * q_m0 / (trace_ms * 1e-3)
         result["roofline_vmem"] = {
-            "kernel": "trace_kernel", "bound": "vector-memory gathers (L1/L2/Infinity-Cache mix)",
+            "kernel": "trace_kernel", "bound": "vector-memory gathers (L1/L2/Infinity-Cache mix), reference rate",
             "achieved": lane_rate, "peak": vmem["ceiling_lane_loads_per_s"], "unit": "16-B lane loads/s",
             "frac": lane_rate / vmem["ceiling_lane_loads_per_s"],
+            "note": "peak = independent one-block-per-lane gathers at this hit mix (tools/td_microbench.hip); "
+                    "shared nodes and same-block node halves let the kernel pass it",
             "mix": {"l1": vmem["fraction_l1"], "l2_hit": vmem["fraction_l2_hit"], "l2_miss": vmem["fraction_l2_miss"]},
             "source": "profiles/r03/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix): " + vmem_why,
         }
