@@ -1017,6 +1017,16 @@ __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, fl
 #define ARX_TRACE_SMALL_BLOCK 256  // block size of launches without the ray pool (0: kBlock)
 #endif
 constexpr int kSmallBlock = ARX_TRACE_SMALL_BLOCK;
+// ... and their node steps per inner iteration / pending leaves before a leaf batch: shorter
+// iterations suit a launch whose time is its longest lane chain (C2 0.419 -> 0.403 ms with 10
+// steps, 0.408 with 8 leaves; C3 unchanged within noise, profiles/r03/ab_tune.txt)
+#ifndef ARX_TRACE_SMALL_STEPS
+#define ARX_TRACE_SMALL_STEPS 10
+#endif
+#ifndef ARX_TRACE_SMALL_LEAF
+#define ARX_TRACE_SMALL_LEAF 8
+#endif
+constexpr int kSmallSteps = ARX_TRACE_SMALL_STEPS, kSmallLeaf = ARX_TRACE_SMALL_LEAF;
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
 constexpr int kSimdsPerCu = 4;
 
@@ -1052,7 +1062,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
         constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
         const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, n_rays);
-        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(g2), dim3(SB),
+        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK>), dim3(g2), dim3(SB),
                            dyn_lds, s, a2);
     } else {
         hipLaunchKernelGGL((trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(grid),
