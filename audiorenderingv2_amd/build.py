@@ -35,6 +35,13 @@ COMMON = [
 ]
 
 
+# Per-file flags.  arx_trace.hip: no SLP vectorisation -- packed f32 VALU (v_pk_add/mul/fma_f32,
+# which the SLP vectoriser forms from the triangle test's and shading's scalar arithmetic) costs more
+# issue cycles than the scalar pairs it replaces (MI355X_MICROARCH.md); C3 trace -2 %, C2 -4 %
+# (profiles/r03/ab_leaf2_noslp.txt).  Same arithmetic, bit-identical results.
+FILE_FLAGS = {"arx_trace.hip": ["-fno-slp-vectorize"]}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):
@@ -48,11 +55,12 @@ def _newest(paths: list[str]) -> float:
 
 def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = (), flags: tuple[str, ...] = ()) -> str:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
-    deps = [src] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "arx.h")]
+    deps = [src, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "arx.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
     lang = ["-x", "hip"]  # host-only TUs too: they use the HIP runtime headers
-    cmd = [hipcc(), *lang, *COMMON, *[f"-D{d}" for d in defines], *flags, "-c", src, "-o", obj]
+    cmd = [hipcc(), *lang, *COMMON, *FILE_FLAGS.get(os.path.basename(src), []), *[f"-D{d}" for d in defines], *flags,
+           "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")

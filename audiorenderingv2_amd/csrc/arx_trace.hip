@@ -31,6 +31,9 @@
 #ifndef ARX_TRACE_BITFLOAT
 #define ARX_TRACE_BITFLOAT 1  // 16-bit planes as the float 2^23 + q built by v_perm (0: u16 -> f32 conversions)
 #endif
+#ifndef ARX_TRACE_LEAF2
+#define ARX_TRACE_LEAF2 1  // a leaf's two triangle records fetched before the first test
+#endif
 #ifndef ARX_TRACE_KEEPHIT
 #define ARX_TRACE_KEEPHIT 1  // the closest hit's V, W, det kept from the leaf test for shading (0: re-test)
 #endif
@@ -259,25 +262,47 @@ struct Best {
 #endif
 };
 
-__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count, Best& b) {
-    for (int k = 0; k < count; ++k) {
-        const float4* tp = base + unit + 3 * k;
-        const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
-        Hit h;
-        if (tri_test(r, p0, p1, p2, h)) {
-            const int id = __float_as_int(p1.w);
-            if (h.t < b.t || (h.t == b.t && id < b.id)) {
-                b.t = h.t;
-                b.id = id;
-                b.unit = unit + 3 * k;
+__device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, float4 p2, int unit, Best& b) {
+    Hit h;
+    if (tri_test(r, p0, p1, p2, h)) {
+        const int id = __float_as_int(p1.w);
+        if (h.t < b.t || (h.t == b.t && id < b.id)) {
+            b.t = h.t;
+            b.id = id;
+            b.unit = unit;
 #if ARX_TRACE_KEEPHIT
-                b.v = h.V;
-                b.w = h.W;
-                b.det = h.det;
+            b.v = h.V;
+            b.w = h.W;
+            b.det = h.det;
 #endif
-            }
         }
     }
+}
+
+__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count, Best& b) {
+#if ARX_TRACE_LEAF2
+    // Leaves hold 1 or 2 triangles (the SBVH's leaf size): both records are fetched before the
+    // first test, so the second fetch's latency hides under the first test.
+    const float4* tp = base + unit;
+    const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
+    float4 q0 = p0, q1 = p1, q2 = p2;
+    if (count > 1) {
+        q0 = tp[3];
+        q1 = tp[4];
+        q2 = tp[5];
+    }
+    take_hit(r, p0, p1, p2, unit, b);
+    if (count > 1) take_hit(r, q0, q1, q2, unit + 3, b);
+    for (int k = 2; k < count; ++k) {
+        const float4* tk = base + unit + 3 * k;
+        take_hit(r, tk[0], tk[1], tk[2], unit + 3 * k, b);
+    }
+#else
+    for (int k = 0; k < count; ++k) {
+        const float4* tp = base + unit + 3 * k;
+        take_hit(r, tp[0], tp[1], tp[2], unit + 3 * k, b);
+    }
+#endif
 }
 // glm-style helpers (glm::dot is x*x + y*y + z*z left to right)
 __device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
