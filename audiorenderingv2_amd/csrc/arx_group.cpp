@@ -115,7 +115,7 @@ arx_status arx_group_create(const arx_config* cfg, const int32_t* devices, int32
         if (hipSetDevice(devs[0]) != hipSuccess || hipEventCreateWithFlags(&g->summed, hipEventDisableTiming) != hipSuccess)
             st = fail(ARX_ERR_HIP, "arx_group_create: event creation failed");
     }
-    if (st == ARX_OK && distinct) {  // RCCL even for one GPU: the same exchange path at every size
+    if (st == ARX_OK && distinct) {  // RCCL even for one GPU: the group collectives work at every size
         g->comms.assign(n_devices, nullptr);
         const ncclResult_t e = ncclCommInitAll(g->comms.data(), n_devices, devs.data());
         if (e != ncclSuccess) {
@@ -292,8 +292,9 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         if (st == ARX_OK) st = arx_trace_rays(r, n * rank / (uint64_t)g->n_ranks, n * (rank + 1) / (uint64_t)g->n_ranks);
         if (st != ARX_OK) return st;
     }
-    // 2. the exchange step: int64 SUM of the histograms
-    if (!g->comms.empty()) {
+    // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:
+    //    its communicator is kept for the group's other collectives, the render skips the no-op)
+    if (!g->comms.empty() && g->n_ranks > 1) {
         ARX_NCCL(ncclGroupStart());
         for (size_t i = 0; i < g->members.size(); ++i) {
             arx_renderer* r = g->members[i];

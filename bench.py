@@ -512,6 +512,25 @@ def main(argv=None) -> int:
 
     value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
+    # frames in flight, before the moving-listener leg: that leg's walk grows the quantization grid
+    # of g for good (the grid only grows), which a fresh second group would not share
+    pipelined = None
+    if not args.no_pipelined:
+        with _stdout_to_stderr():
+            if plan["mode"] == "rank":
+                g2 = RenderGroup.rank(settings, world, rank, uids[1], scene=scene, receiver=receiver)
+            else:
+                g2 = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
+        g2.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        g2.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+        bufs2 = [(DeviceBuffer.from_numpy(m.settings.device, audio_np), DeviceBuffer(m.settings.device, 4 * frames),
+                  DeviceBuffer(m.settings.device, 4 * frames)) for m in g2.members]
+        pipelined = pipelined_leg([g, g2], [bufs, bufs2], frames, args.steps, args.warmup, ranks,
+                                  elapsed / args.steps * 1e3)
+        for b in bufs2:
+            for x in b:
+                x.close()
+        g2.close()
     moving = moving_listener(g, ranks, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
     bpb = bytes_per_bounce(n_tris)
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
@@ -630,23 +649,8 @@ def main(argv=None) -> int:
             shard = total_rays // 8
             result["moving_listener_rank_of_8"] = moving_listener_rank_shape(settings, scene, receiver,
                                                                              args.c5_frames, shard)
-    if not args.no_pipelined:
-        with _stdout_to_stderr():
-            if plan["mode"] == "rank":
-                g2 = RenderGroup.rank(settings, world, rank, uids[1], scene=scene, receiver=receiver)
-            else:
-                g2 = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
-        g2.setEmitterPosInOptix(CONFERENCE_EMITTER)
-        g2.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-        bufs2 = [(DeviceBuffer.from_numpy(m.settings.device, audio_np), DeviceBuffer(m.settings.device, 4 * frames),
-                  DeviceBuffer(m.settings.device, 4 * frames)) for m in g2.members]
-        g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)  # back to the headline pose (C5 moved it)
-        result["pipelined"] = pipelined_leg([g, g2], [bufs, bufs2], frames, args.steps, args.warmup, ranks,
-                                            elapsed / args.steps * 1e3)
-        for b in bufs2:
-            for x in b:
-                x.close()
-        g2.close()
+    if pipelined is not None:
+        result["pipelined"] = pipelined
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
         result["streaming"] = streaming_leg(m0, audio_np, 4096)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
