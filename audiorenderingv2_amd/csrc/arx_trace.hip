@@ -1016,6 +1016,79 @@ __global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float
     out[i] = make_float4(d.x, d.y, d.z, 0.0f);
 }
 
+#ifndef ARX_TRACE_SORT
+#define ARX_TRACE_SORT 0  // design experiment: rays in direction order (bits per octahedral axis; 0 off)
+#endif
+#if ARX_TRACE_SORT
+// Direction-ordered pre-pass (design experiment): the rays of a launch are counting-sorted by the
+// Morton code of their octahedral direction cell, so a wave's lanes start coherent.  A ray's id only
+// picks its direction and the int64 histogram is order-free, so the IR stays bit-identical.
+constexpr int kSortBits = ARX_TRACE_SORT;
+constexpr int kSortBins = 1 << (2 * kSortBits);
+__device__ __forceinline__ uint32_t dir_cell(float3 d) {
+    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float x = d.x / s, y = d.y / s;
+    if (d.z < 0.0f) {
+        const float ox = (1.0f - fabsf(y)) * (x >= 0.0f ? 1.0f : -1.0f);
+        const float oy = (1.0f - fabsf(x)) * (y >= 0.0f ? 1.0f : -1.0f);
+        x = ox;
+        y = oy;
+    }
+    const float m = (float)(1 << kSortBits);
+    const uint32_t u = (uint32_t)min(max((x * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
+    const uint32_t v = (uint32_t)min(max((y * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
+    uint32_t key = 0;
+#pragma unroll
+    for (int b = 0; b < kSortBits; ++b) key |= (((u >> b) & 1u) << (2 * b)) | (((v >> b) & 1u) << (2 * b + 1));
+    return key;
+}
+__global__ void dirs_count_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* tmp, uint32_t* bins,
+                                  unsigned long long* cursor) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *cursor = 0ull;
+    if (i >= count) return;
+    const float3 d = ray_direction(seed, first + i);
+    const uint32_t key = dir_cell(d);
+    tmp[i] = make_float4(d.x, d.y, d.z, __uint_as_float(key));
+    atomicAdd(bins + key, 1u);
+}
+// exclusive scan of kSortBins counts in place, one 1024-lane block
+__global__ void dirs_scan_kernel(uint32_t* bins) {
+    constexpr int per = (kSortBins + 1023) / 1024;
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    uint32_t loc[per];
+    uint32_t sum = 0;
+    for (int k = 0; k < per; ++k) {
+        const int j = t * per + k;
+        loc[k] = j < kSortBins ? bins[j] : 0u;
+        sum += loc[k];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    for (int k = 0; k < per; ++k) {
+        const int j = t * per + k;
+        if (j < kSortBins) bins[j] = run;
+        run += loc[k];
+    }
+}
+__global__ void dirs_scatter_kernel(const float4* __restrict__ tmp, float4* __restrict__ out, uint32_t* bins,
+                                    uint64_t count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float4 v = tmp[i];
+    const uint32_t pos = atomicAdd(bins + __float_as_uint(v.w), 1u);
+    out[pos] = make_float4(v.x, v.y, v.z, 0.0f);
+}
+#endif
+
 __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, float* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -1080,8 +1153,22 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     const bool dyn = n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
     a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
     a2.dyn_chunk = (uint32_t)kDynChunk;
+#if ARX_TRACE_SORT  // the dirs buffer holds 2 * n_rays float4 + kSortBins counters (arx_trace_rays)
+    {
+        float4* sorted = reinterpret_cast<float4*>(const_cast<void*>(args.dirs));
+        float4* tmp = sorted + n_rays;
+        uint32_t* bins = reinterpret_cast<uint32_t*>(tmp + n_rays);
+        (void)hipMemsetAsync(bins, 0, sizeof(uint32_t) * kSortBins, s);
+        const unsigned g = (unsigned)((n_rays + 255) / 256);
+        hipLaunchKernelGGL(dirs_count_kernel, dim3(g), dim3(256), 0, s, args.seed, args.ray_begin, n_rays, tmp, bins,
+                           args.cursor);
+        hipLaunchKernelGGL(dirs_scan_kernel, dim3(1), dim3(1024), 0, s, bins);
+        hipLaunchKernelGGL(dirs_scatter_kernel, dim3(g), dim3(256), 0, s, tmp, sorted, bins, n_rays);
+    }
+#else
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
+#endif
     if (kSmallBlock > 0 && !dyn) {
         // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
