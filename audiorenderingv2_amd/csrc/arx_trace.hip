@@ -32,13 +32,22 @@
 #define ARX_TRACE_BITFLOAT 1  // 16-bit planes as the float 2^23 + q built by v_perm (0: u16 -> f32 conversions)
 #endif
 #ifndef ARX_TRACE_LEAF2
-#define ARX_TRACE_LEAF2 1  // a leaf's two triangle records fetched before the first test
+#define ARX_TRACE_LEAF2 2  // a leaf's two triangle records fetched before the first test (2: no default copy of the second)
 #endif
 #ifndef ARX_TRACE_KEEPHIT
 #define ARX_TRACE_KEEPHIT 1  // the closest hit's V, W, det kept from the leaf test for shading (0: re-test)
 #endif
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
+#endif
+#ifndef ARX_TRACE_LEAFSEL
+#define ARX_TRACE_LEAFSEL 1  // branch-free triangle test + closest-hit update (selects)
+#endif
+#ifndef ARX_TRACE_REFLECT_CR
+#define ARX_TRACE_REFLECT_CR 1  // reflection about the unnormalised face normal (must match the oracle's ORC_REFLECT_CR)
+#endif
+#ifndef ARX_TRACE_SHEAR_RCP
+#define ARX_TRACE_SHEAR_RCP 0  // one division per query setup and per shading (must match the oracle's ORC_SHEAR_RCP)
 #endif
 
 namespace arx {
@@ -170,17 +179,28 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
     int ky = kx + 1;
     if (ky == 3) ky = 0;
     const float dkz = sel3(d.x, d.y, d.z, kz);
+#if !ARX_TRACE_SHEAR_RCP
     if (dkz < 0.0f) {
         const int t = kx;
         kx = ky;
         ky = t;
     }
+#endif
     r.kx = kx;
     r.ky = ky;
     r.kz = kz;
+#if ARX_TRACE_SHEAR_RCP
+    // One division per query: Sz = 1/d[kz], Sx = d[kx]*Sz, Sy = d[ky]*Sz.  The
+    // Woop test's kx/ky swap for d[kz] < 0 is dropped: it negates U, V, W, det and T together, so t
+    // and the barycentric ratios come out bit for bit the same (oracle make_shear).
+    r.sz = 1.0f / dkz;
+    r.sx = sel3(d.x, d.y, d.z, kx) * r.sz;
+    r.sy = sel3(d.x, d.y, d.z, ky) * r.sz;
+#else
     r.sx = sel3(d.x, d.y, d.z, kx) / dkz;
     r.sy = sel3(d.x, d.y, d.z, ky) / dkz;
     r.sz = 1.0f / dkz;
+#endif
     r.op[0] = sel3(o.x, o.y, o.z, kx);
     r.op[1] = sel3(o.x, o.y, o.z, ky);
     r.op[2] = sel3(o.x, o.y, o.z, kz);
@@ -263,6 +283,45 @@ struct Best {
 };
 
 __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, float4 p2, int unit, Best& b) {
+#if ARX_TRACE_LEAFSEL
+    // tri_test's arithmetic without its early exits, the closest-hit update as selects: the branchy
+    // form left the compiler shuffling the Best fields between registers at every join
+    const float Ax = sel3(p0.x, p0.y, p0.z, r.kx) - r.op[0];
+    const float Ay = sel3(p0.x, p0.y, p0.z, r.ky) - r.op[1];
+    const float Az = sel3(p0.x, p0.y, p0.z, r.kz) - r.op[2];
+    const float Bx = sel3(p1.x, p1.y, p1.z, r.kx) - r.op[0];
+    const float By = sel3(p1.x, p1.y, p1.z, r.ky) - r.op[1];
+    const float Bz = sel3(p1.x, p1.y, p1.z, r.kz) - r.op[2];
+    const float Cx = sel3(p2.x, p2.y, p2.z, r.kx) - r.op[0];
+    const float Cy = sel3(p2.x, p2.y, p2.z, r.ky) - r.op[1];
+    const float Cz = sel3(p2.x, p2.y, p2.z, r.kz) - r.op[2];
+    const float ax = Ax - r.sx * Az;
+    const float ay = Ay - r.sy * Az;
+    const float bx = Bx - r.sx * Bz;
+    const float by = By - r.sy * Bz;
+    const float cx = Cx - r.sx * Cz;
+    const float cy = Cy - r.sy * Cz;
+    const float U = cx * by - cy * bx;
+    const float V = ax * cy - ay * cx;
+    const float W = bx * ay - by * ax;
+    const bool edge = !(((U < 0.0f) | (V < 0.0f) | (W < 0.0f)) & ((U > 0.0f) | (V > 0.0f) | (W > 0.0f)));
+    const float det = U + V + W;
+    const float az = r.sz * Az;
+    const float bz = r.sz * Bz;
+    const float cz = r.sz * Cz;
+    const float T = U * az + V * bz + W * cz;
+    const float t = T / det;
+    const int id = __float_as_int(p1.w);
+    const bool take = edge & (det != 0.0f) & (t >= 0.0f) & ((t < b.t) | ((t == b.t) & (id < b.id)));
+    b.t = take ? t : b.t;
+    b.id = take ? id : b.id;
+    b.unit = take ? unit : b.unit;
+#if ARX_TRACE_KEEPHIT
+    b.v = take ? V : b.v;
+    b.w = take ? W : b.w;
+    b.det = take ? det : b.det;
+#endif
+#else
     Hit h;
     if (tri_test(r, p0, p1, p2, h)) {
         const int id = __float_as_int(p1.w);
@@ -277,6 +336,7 @@ __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, flo
 #endif
         }
     }
+#endif
 }
 
 __device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count, Best& b) {
@@ -285,7 +345,11 @@ __device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const
     // first test, so the second fetch's latency hides under the first test.
     const float4* tp = base + unit;
     const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
+#if ARX_TRACE_LEAF2 == 2  // no default copy: the second record is only read where it was loaded
+    float4 q0, q1, q2;
+#else
     float4 q0 = p0, q1 = p1, q2 = p2;
+#endif
     if (count > 1) {
         q0 = tp[3];
         q1 = tp[4];
@@ -357,15 +421,23 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
     // Ng = normalize(cross(P2-P1, P3-P1))  (:75-77)
     const float3 U = sub3(P2, P1), V = sub3(P3, P1);
     const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
+#if !ARX_TRACE_REFLECT_CR
     const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
+#endif
 #if ARX_TRACE_KEEPHIT  // the leaf test's values for this triangle and ray (the same arithmetic)
-    const float bu = best.v / best.det;
-    const float bv = best.w / best.det;
+    const float hv = best.v, hw = best.w, hdet = best.det;
 #else
     Hit h;
     tri_test(r, p0, p1, p2, h);
-    const float bu = h.V / h.det;
-    const float bv = h.W / h.det;
+    const float hv = h.V, hw = h.W, hdet = h.det;
+#endif
+#if ARX_TRACE_SHEAR_RCP  // barycentrics as V * (1/det), W * (1/det): one division
+    const float inv_det = 1.0f / hdet;
+    const float bu = hv * inv_det;
+    const float bv = hw * inv_det;
+#else
+    const float bu = hv / hdet;
+    const float bv = hw / hdet;
 #endif
     const float w0 = (1.0f - bu) - bv;
     const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
@@ -408,8 +480,15 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
         }
         s.depth = -1;
     } else {  // specular reflection + absorption (:173-175)
+#if ARX_TRACE_REFLECT_CR
+        // reflection about the unnormalised normal, dir - (2 (dir . cr) / (cr . cr)) cr: the same
+        // mirror as with normalize(cr) (:75-77, :173) for one division, no square root
+        const float s2 = (2.0f * dot3(s.dir, cr)) / dot3(cr, cr);
+        s.dir = sub3(s.dir, scale3(s2, cr));
+#else
         const float s2 = 2.0f * dot3(s.dir, Ng);
         s.dir = sub3(s.dir, scale3(s2, Ng));
+#endif
         e = e * (1.0f - ab);
         ++s.depth;
     }
