@@ -11,6 +11,7 @@ audiorenderingv2_amd/libarx.so, which travels with the repo snapshot to the GPU 
 from __future__ import annotations
 
 import argparse
+import hashlib
 import concurrent.futures as cf
 import os
 import shutil
@@ -53,14 +54,34 @@ def _newest(paths: list[str]) -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
+# Measurement-only macros: they add counters / per-wave records to the trace kernel but leave its
+# traversal and arithmetic alone, so they do not change the kernel's identity (trace_source_id).
+MEASUREMENT_MACROS = ("ARX_TRACE_COUNT", "ARX_TRACE_PROF")
+
+
+def trace_source_id(defines: tuple[str, ...] = ()) -> str:
+    """64-bit identity of the trace kernel a build compiles: a hash of its source files and of the
+    experiment macros (not the measurement-only ones).  Compiled into the library
+    (arx_trace_kernel_id) and stored in every PMC profile's guard, so bench.py uses a stored
+    profile only for the kernel it was taken of."""
+    h = hashlib.sha1()
+    for f in ("arx_trace.hip", "arx_layout.hpp", "arx_kernels.hpp"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    for d in sorted(d for d in defines if d.split("=")[0] not in MEASUREMENT_MACROS):
+        h.update(b"\0" + d.encode())
+    return "0x" + h.hexdigest()[:16] + "ull"
+
+
 def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = (), flags: tuple[str, ...] = ()) -> str:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     deps = [src, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "arx.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
     lang = ["-x", "hip"]  # host-only TUs too: they use the HIP runtime headers
-    cmd = [hipcc(), *lang, *COMMON, *FILE_FLAGS.get(os.path.basename(src), []), *[f"-D{d}" for d in defines], *flags,
-           "-c", src, "-o", obj]
+    extra = [f"-DARX_TRACE_SRC_ID={trace_source_id(defines)}"] if os.path.basename(src) == "arx_trace.hip" else []
+    cmd = [hipcc(), *lang, *COMMON, *FILE_FLAGS.get(os.path.basename(src), []), *[f"-D{d}" for d in defines], *extra,
+           *flags, "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")

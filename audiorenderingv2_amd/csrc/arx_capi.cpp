@@ -716,6 +716,7 @@ arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) 
 }
 
 int32_t arx_timing_ring(void) { return arx_renderer::kTraceRing; }
+uint64_t arx_trace_kernel_id(void) { return trace_kernel_source_id(); }
 
 int32_t arx_device_count(void) {
     int n = 0;

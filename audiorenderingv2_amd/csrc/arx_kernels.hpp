@@ -26,6 +26,8 @@ hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, 
 // Register allocation of the production trace kernel instance (hipFuncGetAttributes numRegs), the
 // waves per SIMD it admits, and the waves per SIMD the persistent grid is sized for.
 hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target);
+// identity of the trace kernel in this build (build.py trace_source_id; arx_trace_kernel_id)
+uint64_t trace_kernel_source_id();
 
 // ---- moving listener (arx_receiver.hip): transform + fixed-topology refit of the receiver ----
 struct RefitArgs {

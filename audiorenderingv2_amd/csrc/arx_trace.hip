@@ -40,6 +40,9 @@
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
 #endif
+#ifndef ARX_TRACE_LEAFFLAT
+#define ARX_TRACE_LEAFFLAT 0  // leaf step by every lane of a leaf phase, out-of-range buffer loads for the idle ones
+#endif
 #ifndef ARX_TRACE_LEAFSEL
 #define ARX_TRACE_LEAFSEL 1  // branch-free triangle test + closest-hit update (selects)
 #endif
@@ -282,7 +285,8 @@ struct Best {
 #endif
 };
 
-__device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, float4 p2, int unit, Best& b) {
+__device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, float4 p2, int unit, Best& b,
+                                         bool valid = true) {
 #if ARX_TRACE_LEAFSEL
     // tri_test's arithmetic without its early exits, the closest-hit update as selects: the branchy
     // form left the compiler shuffling the Best fields between registers at every join
@@ -312,7 +316,7 @@ __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, flo
     const float T = U * az + V * bz + W * cz;
     const float t = T / det;
     const int id = __float_as_int(p1.w);
-    const bool take = edge & (det != 0.0f) & (t >= 0.0f) & ((t < b.t) | ((t == b.t) & (id < b.id)));
+    const bool take = valid & edge & (det != 0.0f) & (t >= 0.0f) & ((t < b.t) | ((t == b.t) & (id < b.id)));
     b.t = take ? t : b.t;
     b.id = take ? id : b.id;
     b.unit = take ? unit : b.unit;
@@ -796,6 +800,47 @@ __device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, cons
     }
 }
 
+#if ARX_TRACE_LEAFFLAT
+static_assert(ARX_TRACE_LEAFSEL, "the flat leaf step needs the branch-free triangle test");
+// Leaf step run by every lane of a leaf phase, no divergent branch (ARX_TRACE_LEAFFLAT): lanes
+// without a pending leaf, and the second record of a one-triangle leaf, load through a buffer
+// offset past the resource's range, which returns zeros without a memory access, and their tests
+// are masked off.  Straight-line code lets the closest-hit state stay in its registers (the
+// divergent form made the compiler copy it in and out at every join).
+__device__ __forceinline__ float4 tri_unit(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
+template <int FMT, typename Stack>
+__device__ __forceinline__ void leaf_step_flat(__amdgpu_buffer_rsrc_t trs, const float4* __restrict__ tbase, const Ray& r,
+                                               Trav& t, const Stack& stk) {
+    const bool lf = t.node <= -2;
+    const int v = ~t.node;
+    const int unit = FMT == kFmtW4 ? (v >> 2) : 3 * (v >> 4);
+    const int count = lf ? (FMT == kFmtW4 ? (v & 3) : (v & 15)) : 0;
+    constexpr uint32_t kNoLoad = 0x80000000u;  // > num_records (0x7fffffff): zeros, no access
+    const uint32_t o0 = count > 0 ? (uint32_t)unit * 16u : kNoLoad;
+    const uint32_t o1 = count > 1 ? (uint32_t)(unit + 3) * 16u : kNoLoad;
+    const float4 p0 = tri_unit(trs, o0), p1 = tri_unit(trs, o0 + 16u), p2 = tri_unit(trs, o0 + 32u);
+    const float4 q0 = tri_unit(trs, o1), q1 = tri_unit(trs, o1 + 16u), q2 = tri_unit(trs, o1 + 32u);
+    take_hit(r, p0, p1, p2, unit, t.best, count > 0);
+    take_hit(r, q0, q1, q2, unit + 3, t.best, count > 1);
+    for (int k = 2; k < count; ++k) {  // leaves past 2 triangles only below the builder's depth cap
+        const float4* tk = tbase + unit + 3 * k;
+        take_hit(r, tk[0], tk[1], tk[2], unit + 3 * k, t.best);
+    }
+    const int sp = t.sp;
+    int top = stk.below(sp);
+    asm volatile("" : "+v"(top));
+    if constexpr (Stack::kSentinel) {
+        t.node = lf ? top : t.node;
+        t.sp = lf ? sp - 1 : sp;
+    } else {
+        t.node = lf ? (sp > 0 ? top : -1) : t.node;
+        t.sp = lf ? max(sp - 1, 0) : sp;
+    }
+}
+#endif
+
 // Highest VGPR the trace kernel claims, so that its allocation (granule 8) admits exactly
 // ARX_TRACE_WAVES waves per SIMD: 5 -> 88 VGPRs (512/88 = 5.8), 4 -> 104, 6 -> 80.  Every wave of
 // a persistent launch owns an equal share of the rays, so a SIMD holding one wave more than the
@@ -875,6 +920,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     }
     const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf) : (Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes));
     const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
+#if ARX_TRACE_LEAFFLAT
+    const __amdgpu_buffer_rsrc_t trs = buffer_rsrc(tbase);
+#endif
     const uint64_t n = a.ray_end - a.ray_begin;
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane(gid >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
@@ -1026,12 +1074,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                 ++pf[6];
                 pf[7] += __popcll(m_leaf);
 #endif
+#if ARX_TRACE_LEAFFLAT
+#if ARX_TRACE_COUNT
+                if (t.node <= -2) n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
+#endif
+                leaf_step_flat<FMT>(trs, tbase, r, t, stk);
+#else
                 if (t.node <= -2) {
 #if ARX_TRACE_COUNT
                     n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
 #endif
                     leaf_step<FMT>(tbase, r, t, stk);
                 }
+#endif
             }
         }
     }
@@ -1277,6 +1332,11 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_g
     if (a.qnodes) return gstack ? launch<kFmtQ16, true>(a, cus, s) : launch<kFmtQ16, false>(a, cus, s);
     return gstack ? launch<kFmtF32, true>(a, cus, s) : launch<kFmtF32, false>(a, cus, s);
 }
+
+#ifndef ARX_TRACE_SRC_ID
+#define ARX_TRACE_SRC_ID 0ull  // set by build.py: hash of this kernel's sources and experiment macros
+#endif
+uint64_t trace_kernel_source_id() { return ARX_TRACE_SRC_ID; }
 
 hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;

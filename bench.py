@@ -364,15 +364,17 @@ def load_profile(name: str) -> dict | None:
 
 
 def profile_guard(prof: dict | None, workload: str, stats: dict,
-                  keys: tuple = ("workload", "tree_hash", "trace_vgprs")) -> tuple[dict | None, str]:
+                  keys: tuple = ("workload", "tree_hash", "trace_vgprs", "trace_kernel_id")) -> tuple[dict | None, str]:
     """A stored PMC-derived profile applies to this run only if it was taken on the same workload,
-    the same scene tree (content hash) and the same trace kernel build (register allocation): the
-    counters cannot be read inside this run, and a stale file must not pass as a measurement.
-    (Per-query lane counts come from a separate counting build: they are guarded by the tree only.)"""
+    the same scene tree (content hash) and the same trace kernel (source identity, arx_trace_kernel_id,
+    and register allocation): the counters cannot be read inside this run, and a stale file must not
+    pass as a measurement.  (Per-query lane counts come from a separate counting build of the same
+    kernel source: they are guarded by the tree and the kernel identity.)"""
+    from audiorenderingv2_amd._lib import lib
     if prof is None:
         return None, "missing"
     want = {"workload": workload, "tree_hash": f"{int(stats['tree_hash']):016x}",
-            "trace_vgprs": int(stats["trace_vgprs"])}
+            "trace_vgprs": int(stats["trace_vgprs"]), "trace_kernel_id": f"{int(lib().arx_trace_kernel_id()):016x}"}
     want = {k: want[k] for k in keys}
     bad = [k for k, v in want.items() if prof.get(k) != v]
     if bad:
@@ -536,7 +538,7 @@ def main(argv=None) -> int:
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
     traffic, traffic_why = profile_guard(load_profile(os.path.join("r03", "trace_traffic.json")), args.workload, st0)
     counts, counts_why = profile_guard(load_profile(os.path.join("r03", "trace_counts_c3.json")), args.workload, st0,
-                                       ("workload", "tree_hash"))
+                                       ("workload", "tree_hash", "trace_kernel_id"))
     td, td_why = profile_guard(load_profile(os.path.join("r03", "trace_td_c3.json")), args.workload, st0)
     vmem, vmem_why = profile_guard(load_profile(os.path.join("r03", "trace_vmem_ceiling.json")), args.workload, st0)
     conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02m.json"))

@@ -174,6 +174,12 @@ arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 /* Capacity of the per-launch timing rings above (launches kept). */
 int32_t arx_timing_ring(void);
+
+/* Identity of the trace kernel compiled into this library: a hash of its sources and experiment
+ * macros (build.py trace_source_id).  Stored PMC profiles carry it with the tree hash and VGPR
+ * count, and bench.py uses a stored profile only when all three match its own run.  No
+ * reference counterpart (measurement plumbing). */
+uint64_t arx_trace_kernel_id(void);
 /* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */

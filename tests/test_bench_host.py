@@ -68,13 +68,18 @@ def test_unique_id_reaches_every_rank_of_one_launch(tmp_path, monkeypatch):
 
 
 def test_profile_guard():
+    from audiorenderingv2_amd._lib import lib
+    kid = f"{int(lib().arx_trace_kernel_id()):016x}"
     st = {"tree_hash": 0xABC, "trace_vgprs": 88}
-    good = {"workload": "c3", "tree_hash": "0000000000000abc", "trace_vgprs": 88, "bytes_per_launch": 1.0}
+    good = {"workload": "c3", "tree_hash": "0000000000000abc", "trace_vgprs": 88, "trace_kernel_id": kid,
+            "bytes_per_launch": 1.0}
     assert bench.profile_guard(good, "c3", st)[0] is good
     assert bench.profile_guard(good, "c2", st)[0] is None
     assert bench.profile_guard(dict(good, tree_hash="0000000000000abd"), "c3", st)[0] is None
     p, why = bench.profile_guard(dict(good, trace_vgprs=80), "c3", st)
     assert p is None and "trace_vgprs" in why
+    p, why = bench.profile_guard(dict(good, trace_kernel_id="0123456789abcdef"), "c3", st)
+    assert p is None and "trace_kernel_id" in why  # another kernel's counters, same tree and VGPRs
     assert bench.profile_guard(None, "c3", st) == (None, "missing")
 
 

@@ -32,6 +32,18 @@ def test_library_exports_every_declared_symbol():
     assert L.arx_abi_version() == 2
 
 
+def test_trace_kernel_id_is_the_build_source_hash():
+    """The library reports the identity build.py hashed from the trace kernel's sources (the guard
+    of every stored PMC profile); an experiment macro gives another identity, a measurement-only
+    macro does not."""
+    from audiorenderingv2_amd import build
+    kid = int(_lib.lib().arx_trace_kernel_id())
+    assert kid != 0
+    assert kid == int(build.trace_source_id()[:-3], 16)
+    assert build.trace_source_id(("ARX_TRACE_COUNT=1",)) == build.trace_source_id()
+    assert build.trace_source_id(("ARX_TRACE_LEAFFLAT=1",)) != build.trace_source_id()
+
+
 def test_status_strings_and_errors():
     L = _lib.lib()
     assert L.arx_status_string(0) == b"ok"

@@ -53,7 +53,7 @@ def main() -> int:
     if len(sys.argv) > 4:
         with open(sys.argv[4]) as fh:
             guard = json.load(fh)
-        out.update({k: guard[k] for k in ("tree_hash", "trace_vgprs") if k in guard})
+        out.update({k: guard[k] for k in ("tree_hash", "trace_vgprs", "trace_kernel_id") if k in guard})
     path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r03", "trace_traffic.json")
     with open(path, "w") as fh:

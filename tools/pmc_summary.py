@@ -39,7 +39,7 @@ def main():
         g = c["GRBM_GUI_ACTIVE"] / 8
         guard = json.load(open(sys.argv[3]))
         out = {"workload": guard.get("workload"), "tree_hash": guard.get("tree_hash"),
-               "trace_vgprs": guard.get("trace_vgprs"), "kernel": "trace_kernel (16-bit BVH2, LDS stack)",
+               "trace_vgprs": guard.get("trace_vgprs"), "trace_kernel_id": guard.get("trace_kernel_id"), "kernel": "trace_kernel (16-bit BVH2, LDS stack)",
                "td_busy_per_cu_cycle": c["TD_TD_BUSY_sum"] / cus / g, "ta_busy_per_cu_cycle": c["TA_TA_BUSY_sum"] / cus / g,
                "l2_hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]),
                "sq_wait_any_per_wave_cycle": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],

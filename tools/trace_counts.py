@@ -31,6 +31,7 @@ q, steps, tris = c[0], c[4], c[5]
 loads = 2 * steps + 3 * tris + 3 * q + 1 * 10**6
 st = r.stats()
 # guard: the same tree as the product run (the counting build's kernel differs, its tree does not)
-print(json.dumps({"workload": "c3", "tree_hash": f"{int(st['tree_hash']):016x}", "queries": q, "node_steps": steps,
+print(json.dumps({"workload": "c3", "tree_hash": f"{int(st['tree_hash']):016x}",
+                  "trace_kernel_id": f"{int(lib().arx_trace_kernel_id()):016x}", "queries": q, "node_steps": steps,
                   "tri_tests": tris, "steps_per_query": steps / q, "tri_tests_per_query": tris / q,
                   "lane_loads_16B_per_query": loads / q, "trace_ms_counting_build": ms}))

@@ -55,7 +55,7 @@ def main():
     guard = json.load(open(sys.argv[4])) if len(sys.argv) > 4 else {}
     print(json.dumps({
         "workload": c["workload"],
-        **{k: guard[k] for k in ("tree_hash", "trace_vgprs") if k in guard},
+        **{k: guard[k] for k in ("tree_hash", "trace_vgprs", "trace_kernel_id") if k in guard},
         "lane_loads_per_launch": lane_loads,
         "fraction_l1": f_l1, "fraction_l2_hit": f_l2hit, "fraction_l2_miss": f_mall,
         "rate_l1_lane_loads_per_s": r1, "rate_l2_lane_loads_per_s": r2, "rate_mall_lane_loads_per_s": r3,
