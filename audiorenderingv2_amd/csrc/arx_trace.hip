@@ -40,8 +40,11 @@
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
 #endif
+#ifndef ARX_TRACE_INPLACE
+#define ARX_TRACE_INPLACE 0  // the branch-free leaf updates written in place (sel_inplace)
+#endif
 #ifndef ARX_TRACE_LEAFFLAT
-#define ARX_TRACE_LEAFFLAT 0  // leaf step by every lane of a leaf phase, out-of-range buffer loads for the idle ones
+#define ARX_TRACE_LEAFFLAT 1  // leaf step by every lane of a leaf phase, out-of-range buffer loads for the idle ones
 #endif
 #ifndef ARX_TRACE_LEAFSEL
 #define ARX_TRACE_LEAFSEL 1  // branch-free triangle test + closest-hit update (selects)
@@ -274,6 +277,18 @@ __device__ __forceinline__ bool tri_test(const Ray& r, float4 p0, float4 p1, flo
 
 // Triangles [unit, unit + 3*count) of a 16-B-unit array (TriRec = 3 units): d_tris for the BVH2
 // trees, the CW4 buffer's leaf blocks for CW4.  best = the closest hit's unit.
+#if ARX_TRACE_INPLACE
+// x = lane in m ? v : x, written back into x's own register: the leaf path's updates of the loop-
+// carried traversal state then leave it where the node path keeps it, so the join of the two needs
+// no register copies (the compiler's select allocated fresh registers and copied at every join).
+__device__ __forceinline__ void sel_inplace(float& x, float v, uint64_t m) {
+    asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(v), "s"(m));
+}
+__device__ __forceinline__ void sel_inplace(int& x, int v, uint64_t m) {
+    asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(v), "s"(m));
+}
+#endif
+
 // The closest hit so far of one query: t, triangle id (tie-break), the TriRec's unit (-1 none) and,
 // with ARX_TRACE_KEEPHIT, the test's V, W and det, so shade() needs no second triangle test.
 struct Best {
@@ -317,6 +332,17 @@ __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, flo
     const float t = T / det;
     const int id = __float_as_int(p1.w);
     const bool take = valid & edge & (det != 0.0f) & (t >= 0.0f) & ((t < b.t) | ((t == b.t) & (id < b.id)));
+#if ARX_TRACE_INPLACE
+    const uint64_t m = __builtin_amdgcn_ballot_w64(take);
+    sel_inplace(b.t, t, m);
+    sel_inplace(b.id, id, m);
+    sel_inplace(b.unit, unit, m);
+#if ARX_TRACE_KEEPHIT
+    sel_inplace(b.v, V, m);
+    sel_inplace(b.w, W, m);
+    sel_inplace(b.det, det, m);
+#endif
+#else
     b.t = take ? t : b.t;
     b.id = take ? id : b.id;
     b.unit = take ? unit : b.unit;
@@ -324,6 +350,7 @@ __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, flo
     b.v = take ? V : b.v;
     b.w = take ? W : b.w;
     b.det = take ? det : b.det;
+#endif
 #endif
 #else
     Hit h;
@@ -824,19 +851,20 @@ __device__ __forceinline__ void leaf_step_flat(__amdgpu_buffer_rsrc_t trs, const
     const float4 q0 = tri_unit(trs, o1), q1 = tri_unit(trs, o1 + 16u), q2 = tri_unit(trs, o1 + 32u);
     take_hit(r, p0, p1, p2, unit, t.best, count > 0);
     take_hit(r, q0, q1, q2, unit + 3, t.best, count > 1);
-    for (int k = 2; k < count; ++k) {  // leaves past 2 triangles only below the builder's depth cap
-        const float4* tk = tbase + unit + 3 * k;
-        take_hit(r, tk[0], tk[1], tk[2], unit + 3 * k, t.best);
-    }
+    // A leaf of more than 2 triangles (only below the builder's depth cap) continues as the same leaf
+    // two triangles on, instead of a loop here: the step stays loop-free (a divergent loop in it
+    // made the compiler move the closest-hit state into other registers and back at every join).
+    const bool more = count > 2;
+    const int rest = FMT == kFmtW4 ? ~((unit + 6) * 4 + (count - 2)) : ~(((unit / 3) + 2) * 16 + (count - 2));
     const int sp = t.sp;
     int top = stk.below(sp);
     asm volatile("" : "+v"(top));
     if constexpr (Stack::kSentinel) {
-        t.node = lf ? top : t.node;
-        t.sp = lf ? sp - 1 : sp;
+        t.node = lf ? (more ? rest : top) : t.node;
+        t.sp = (lf & !more) ? sp - 1 : sp;
     } else {
-        t.node = lf ? (sp > 0 ? top : -1) : t.node;
-        t.sp = lf ? max(sp - 1, 0) : sp;
+        t.node = lf ? (more ? rest : (sp > 0 ? top : -1)) : t.node;
+        t.sp = (lf & !more) ? max(sp - 1, 0) : sp;
     }
 }
 #endif
