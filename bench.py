@@ -633,6 +633,14 @@ def main(argv=None) -> int:
             "unit": "TD busy cycles per CU-cycle", "frac": td["td_busy_per_cu_cycle"],
             "ta_busy": td["ta_busy_per_cu_cycle"], "source": td["source"] + ": " + td_why,
         }
+        if "valu_busy_per_simd_cycle" in td:
+            # the second unit the trace kernel saturates: VALU issue (a wave64 instruction holds a
+            # 16-lane SIMD 4 cycles), SQ_INSTS_VALU x 4 over the SIMDs' cycles in the PMC run
+            result["roofline_valu"] = {
+                "kernel": "trace_kernel", "bound": "valu issue", "achieved": td["valu_busy_per_simd_cycle"],
+                "peak": 1.0, "unit": "VALU-busy cycles per SIMD-cycle", "frac": td["valu_busy_per_simd_cycle"],
+                "valu_instructions_per_launch": td["valu_instructions"], "source": td["source"] + ": " + td_why,
+            }
     else:
         result["roofline_td"] = None
         result["roofline_td_why"] = td_why

@@ -45,6 +45,10 @@ def main():
                "sq_wait_any_per_wave_cycle": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"],
                "valu_active_per_wave_cycle": c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"],
                "valu_instructions": c["SQ_INSTS_VALU"],
+               # a wave64 VALU instruction holds a 16-lane SIMD for 4 cycles: the SIMDs' VALU issue
+               # fraction over the kernel's cycles (GRBM_GUI_ACTIVE / 8 = cycles per XCD)
+               "kernel_cycles_per_xcd": g,
+               "valu_busy_per_simd_cycle": c["SQ_INSTS_VALU"] * 4.0 / (cus * 4) / g,
                "source": sys.argv[2]}
         with open(sys.argv[2], "w") as fh:
             json.dump(out, fh, indent=1)
