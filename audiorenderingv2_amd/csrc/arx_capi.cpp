@@ -1065,11 +1065,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         if (r->d_dirs) ARX_HIP(hipFree(r->d_dirs));
         r->d_dirs = nullptr;
         r->dirs_cap = 0;
-#if defined(ARX_TRACE_SORT) && ARX_TRACE_SORT  // design experiment: sorted copy + scratch + bin counters (launch_trace)
-        ARX_HIP(hipMalloc(&r->d_dirs, (ray_end - ray_begin) * 32 + ((size_t)4 << (2 * ARX_TRACE_SORT))));
-#else
         ARX_HIP(hipMalloc(&r->d_dirs, (ray_end - ray_begin) * 16));
-#endif
         r->dirs_cap = ray_end - ray_begin;
     }
     a.dirs = r->d_dirs;

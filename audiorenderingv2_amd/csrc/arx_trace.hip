@@ -31,29 +31,8 @@
 #ifndef ARX_TRACE_BITFLOAT
 #define ARX_TRACE_BITFLOAT 1  // 16-bit planes as the float 2^23 + q built by v_perm (0: u16 -> f32 conversions)
 #endif
-#ifndef ARX_TRACE_LEAF2
-#define ARX_TRACE_LEAF2 2  // a leaf's two triangle records fetched before the first test (2: no default copy of the second)
-#endif
-#ifndef ARX_TRACE_KEEPHIT
-#define ARX_TRACE_KEEPHIT 1  // the closest hit's V, W, det kept from the leaf test for shading (0: re-test)
-#endif
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
-#endif
-#ifndef ARX_TRACE_INPLACE
-#define ARX_TRACE_INPLACE 0  // the branch-free leaf updates written in place (sel_inplace)
-#endif
-#ifndef ARX_TRACE_LEAFFLAT
-#define ARX_TRACE_LEAFFLAT 1  // leaf step by every lane of a leaf phase, out-of-range buffer loads for the idle ones
-#endif
-#ifndef ARX_TRACE_LEAFSEL
-#define ARX_TRACE_LEAFSEL 1  // branch-free triangle test + closest-hit update (selects)
-#endif
-#ifndef ARX_TRACE_REFLECT_CR
-#define ARX_TRACE_REFLECT_CR 1  // reflection about the unnormalised face normal (must match the oracle's ORC_REFLECT_CR)
-#endif
-#ifndef ARX_TRACE_SHEAR_RCP
-#define ARX_TRACE_SHEAR_RCP 0  // one division per query setup and per shading (must match the oracle's ORC_SHEAR_RCP)
 #endif
 
 namespace arx {
@@ -185,28 +164,17 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
     int ky = kx + 1;
     if (ky == 3) ky = 0;
     const float dkz = sel3(d.x, d.y, d.z, kz);
-#if !ARX_TRACE_SHEAR_RCP
     if (dkz < 0.0f) {
         const int t = kx;
         kx = ky;
         ky = t;
     }
-#endif
     r.kx = kx;
     r.ky = ky;
     r.kz = kz;
-#if ARX_TRACE_SHEAR_RCP
-    // One division per query: Sz = 1/d[kz], Sx = d[kx]*Sz, Sy = d[ky]*Sz.  The
-    // Woop test's kx/ky swap for d[kz] < 0 is dropped: it negates U, V, W, det and T together, so t
-    // and the barycentric ratios come out bit for bit the same (oracle make_shear).
-    r.sz = 1.0f / dkz;
-    r.sx = sel3(d.x, d.y, d.z, kx) * r.sz;
-    r.sy = sel3(d.x, d.y, d.z, ky) * r.sz;
-#else
     r.sx = sel3(d.x, d.y, d.z, kx) / dkz;
     r.sy = sel3(d.x, d.y, d.z, ky) / dkz;
     r.sz = 1.0f / dkz;
-#endif
     r.op[0] = sel3(o.x, o.y, o.z, kx);
     r.op[1] = sel3(o.x, o.y, o.z, ky);
     r.op[2] = sel3(o.x, o.y, o.z, kz);
@@ -232,79 +200,23 @@ __device__ __forceinline__ void setup_ray(Ray& r, float3 o, float3 d) {
     }
 }
 
-// Watertight ray/triangle test (Woop, Benthin, Wald 2013); t >= 0 (optixTrace tmin 0).
-// Vertex components are selected by (kx,ky,kz) then differenced against the permuted
-// origin: the same values as A[k] = v[k] - o[k] indexed afterwards (oracle order).
-struct Hit {
-    float U, V, W, det, t;
-};
-
-__device__ __forceinline__ bool tri_test(const Ray& r, float4 p0, float4 p1, float4 p2, Hit& h) {
-    const float Ax = sel3(p0.x, p0.y, p0.z, r.kx) - r.op[0];
-    const float Ay = sel3(p0.x, p0.y, p0.z, r.ky) - r.op[1];
-    const float Az = sel3(p0.x, p0.y, p0.z, r.kz) - r.op[2];
-    const float Bx = sel3(p1.x, p1.y, p1.z, r.kx) - r.op[0];
-    const float By = sel3(p1.x, p1.y, p1.z, r.ky) - r.op[1];
-    const float Bz = sel3(p1.x, p1.y, p1.z, r.kz) - r.op[2];
-    const float Cx = sel3(p2.x, p2.y, p2.z, r.kx) - r.op[0];
-    const float Cy = sel3(p2.x, p2.y, p2.z, r.ky) - r.op[1];
-    const float Cz = sel3(p2.x, p2.y, p2.z, r.kz) - r.op[2];
-    const float ax = Ax - r.sx * Az;
-    const float ay = Ay - r.sy * Az;
-    const float bx = Bx - r.sx * Bz;
-    const float by = By - r.sy * Bz;
-    const float cx = Cx - r.sx * Cz;
-    const float cy = Cy - r.sy * Cz;
-    const float U = cx * by - cy * bx;
-    const float V = ax * cy - ay * cx;
-    const float W = bx * ay - by * ax;
-    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
-    const float det = U + V + W;
-    if (det == 0.0f) return false;
-    const float az = r.sz * Az;
-    const float bz = r.sz * Bz;
-    const float cz = r.sz * Cz;
-    const float T = U * az + V * bz + W * cz;
-    const float t = T / det;
-    if (!(t >= 0.0f)) return false;
-    h.U = U;
-    h.V = V;
-    h.W = W;
-    h.det = det;
-    h.t = t;
-    return true;
-}
-
-// Triangles [unit, unit + 3*count) of a 16-B-unit array (TriRec = 3 units): d_tris for the BVH2
-// trees, the CW4 buffer's leaf blocks for CW4.  best = the closest hit's unit.
-#if ARX_TRACE_INPLACE
-// x = lane in m ? v : x, written back into x's own register: the leaf path's updates of the loop-
-// carried traversal state then leave it where the node path keeps it, so the join of the two needs
-// no register copies (the compiler's select allocated fresh registers and copied at every join).
-__device__ __forceinline__ void sel_inplace(float& x, float v, uint64_t m) {
-    asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(v), "s"(m));
-}
-__device__ __forceinline__ void sel_inplace(int& x, int v, uint64_t m) {
-    asm("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x) : "v"(v), "s"(m));
-}
-#endif
-
-// The closest hit so far of one query: t, triangle id (tie-break), the TriRec's unit (-1 none) and,
-// with ARX_TRACE_KEEPHIT, the test's V, W and det, so shade() needs no second triangle test.
+// The closest hit so far of one query: t, triangle id (tie-break), the TriRec's unit (-1 none) and
+// the test's V, W and det, so shade() needs no second triangle test.
 struct Best {
     float t;
     int id;
     int unit;
-#if ARX_TRACE_KEEPHIT
     float v, w, det;
-#endif
 };
 
+// Watertight ray/triangle test (Woop, Benthin, Wald 2013), t >= 0 (optixTrace tmin 0), and the
+// closest-hit update (ties to the lowest id) for a lane where `valid`.  Vertex components are selected
+// by (kx,ky,kz) then differenced against the permuted origin: the same values as A[k] = v[k] - o[k]
+// indexed afterwards (oracle order).  Branch-free: the early exits of the textbook form and an
+// if-based update left the compiler shuffling the Best fields between registers at every join
+// (DESIGN.md section 6.3).
 __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, float4 p2, int unit, Best& b,
-                                         bool valid = true) {
-#if ARX_TRACE_LEAFSEL
-    // tri_test's arithmetic without its early exits, the closest-hit update as selects: the branchy
-    // form left the compiler shuffling the Best fields between registers at every join
+                                         bool valid) {
     const float Ax = sel3(p0.x, p0.y, p0.z, r.kx) - r.op[0];
     const float Ay = sel3(p0.x, p0.y, p0.z, r.ky) - r.op[1];
     const float Az = sel3(p0.x, p0.y, p0.z, r.kz) - r.op[2];
@@ -332,73 +244,14 @@ __device__ __forceinline__ void take_hit(const Ray& r, float4 p0, float4 p1, flo
     const float t = T / det;
     const int id = __float_as_int(p1.w);
     const bool take = valid & edge & (det != 0.0f) & (t >= 0.0f) & ((t < b.t) | ((t == b.t) & (id < b.id)));
-#if ARX_TRACE_INPLACE
-    const uint64_t m = __builtin_amdgcn_ballot_w64(take);
-    sel_inplace(b.t, t, m);
-    sel_inplace(b.id, id, m);
-    sel_inplace(b.unit, unit, m);
-#if ARX_TRACE_KEEPHIT
-    sel_inplace(b.v, V, m);
-    sel_inplace(b.w, W, m);
-    sel_inplace(b.det, det, m);
-#endif
-#else
     b.t = take ? t : b.t;
     b.id = take ? id : b.id;
     b.unit = take ? unit : b.unit;
-#if ARX_TRACE_KEEPHIT
     b.v = take ? V : b.v;
     b.w = take ? W : b.w;
     b.det = take ? det : b.det;
-#endif
-#endif
-#else
-    Hit h;
-    if (tri_test(r, p0, p1, p2, h)) {
-        const int id = __float_as_int(p1.w);
-        if (h.t < b.t || (h.t == b.t && id < b.id)) {
-            b.t = h.t;
-            b.id = id;
-            b.unit = unit;
-#if ARX_TRACE_KEEPHIT
-            b.v = h.V;
-            b.w = h.W;
-            b.det = h.det;
-#endif
-        }
-    }
-#endif
 }
 
-__device__ __forceinline__ void leaf_hits(const float4* __restrict__ base, const Ray& r, int unit, int count, Best& b) {
-#if ARX_TRACE_LEAF2
-    // Leaves hold 1 or 2 triangles (the SBVH's leaf size): both records are fetched before the
-    // first test, so the second fetch's latency hides under the first test.
-    const float4* tp = base + unit;
-    const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
-#if ARX_TRACE_LEAF2 == 2  // no default copy: the second record is only read where it was loaded
-    float4 q0, q1, q2;
-#else
-    float4 q0 = p0, q1 = p1, q2 = p2;
-#endif
-    if (count > 1) {
-        q0 = tp[3];
-        q1 = tp[4];
-        q2 = tp[5];
-    }
-    take_hit(r, p0, p1, p2, unit, b);
-    if (count > 1) take_hit(r, q0, q1, q2, unit + 3, b);
-    for (int k = 2; k < count; ++k) {
-        const float4* tk = base + unit + 3 * k;
-        take_hit(r, tk[0], tk[1], tk[2], unit + 3 * k, b);
-    }
-#else
-    for (int k = 0; k < count; ++k) {
-        const float4* tp = base + unit + 3 * k;
-        take_hit(r, tp[0], tp[1], tp[2], unit + 3 * k, b);
-    }
-#endif
-}
 // glm-style helpers (glm::dot is x*x + y*y + z*z left to right)
 __device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ float3 sub3(float3 a, float3 b) { return make_float3(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -443,7 +296,7 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
         s.depth = -1;
         return;
     }
-    const float4* tp = tbase + hit;  // hit = the triangle's 16-B unit (leaf_hits)
+    const float4* tp = tbase + hit;  // hit = the triangle's 16-B unit (leaf_step)
     const float4 p0 = tp[0], p1 = tp[1], p2 = tp[2];
     const float3 P1 = make_float3(p0.x, p0.y, p0.z);
     const float3 P2 = make_float3(p1.x, p1.y, p1.z);
@@ -452,24 +305,9 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
     // Ng = normalize(cross(P2-P1, P3-P1))  (:75-77)
     const float3 U = sub3(P2, P1), V = sub3(P3, P1);
     const float3 cr = make_float3(U.y * V.z - V.y * U.z, U.z * V.x - V.z * U.x, U.x * V.y - V.x * U.y);
-#if !ARX_TRACE_REFLECT_CR
-    const float3 Ng = scale3(1.0f / sqrtf(dot3(cr, cr)), cr);
-#endif
-#if ARX_TRACE_KEEPHIT  // the leaf test's values for this triangle and ray (the same arithmetic)
     const float hv = best.v, hw = best.w, hdet = best.det;
-#else
-    Hit h;
-    tri_test(r, p0, p1, p2, h);
-    const float hv = h.V, hw = h.W, hdet = h.det;
-#endif
-#if ARX_TRACE_SHEAR_RCP  // barycentrics as V * (1/det), W * (1/det): one division
-    const float inv_det = 1.0f / hdet;
-    const float bu = hv * inv_det;
-    const float bv = hw * inv_det;
-#else
     const float bu = hv / hdet;
     const float bv = hw / hdet;
-#endif
     const float w0 = (1.0f - bu) - bv;
     const float3 P = add3(add3(scale3(w0, P1), scale3(bu, P2)), scale3(bv, P3));  // :81
     const float3 seg = sub3(P, s.pos);
@@ -511,15 +349,10 @@ __device__ __forceinline__ void shade(const TraceArgs& a, const float4* __restri
         }
         s.depth = -1;
     } else {  // specular reflection + absorption (:173-175)
-#if ARX_TRACE_REFLECT_CR
         // reflection about the unnormalised normal, dir - (2 (dir . cr) / (cr . cr)) cr: the same
         // mirror as with normalize(cr) (:75-77, :173) for one division, no square root
         const float s2 = (2.0f * dot3(s.dir, cr)) / dot3(cr, cr);
         s.dir = sub3(s.dir, scale3(s2, cr));
-#else
-        const float s2 = 2.0f * dot3(s.dir, Ng);
-        s.dir = sub3(s.dir, scale3(s2, Ng));
-#endif
         e = e * (1.0f - ab);
         ++s.depth;
     }
@@ -808,28 +641,7 @@ __device__ __forceinline__ void node_step_w4(const Ray& r, float oix, float oiy,
     t.sp = hits > 0 ? sp + hits - 1 : sp_pop;
 }
 
-// Leaf step: test the pending leaf's triangles, then pop the next entry.
-// BVH2 leaf codes ~(first*16 + count) (first = TriRec index); CW4 leaf codes ~(unit*4 + count).
-template <int FMT, typename Stack>
-__device__ __forceinline__ void leaf_step(const float4* __restrict__ tbase, const Ray& r, Trav& t, const Stack& stk) {
-    const int v = ~t.node;
-    if constexpr (FMT == kFmtW4) leaf_hits(tbase, r, v >> 2, v & 3, t.best);
-    else leaf_hits(tbase, r, 3 * (v >> 4), v & 15, t.best);
-    const int sp = t.sp;
-    int top = stk.below(sp);
-    asm volatile("" : "+v"(top));
-    if constexpr (Stack::kSentinel) {
-        t.node = top;
-        t.sp = sp - 1;
-    } else {
-        t.node = sp > 0 ? top : -1;
-        t.sp = max(sp - 1, 0);
-    }
-}
-
-#if ARX_TRACE_LEAFFLAT
-static_assert(ARX_TRACE_LEAFSEL, "the flat leaf step needs the branch-free triangle test");
-// Leaf step run by every lane of a leaf phase, no divergent branch (ARX_TRACE_LEAFFLAT): lanes
+// Leaf step, run by every lane of a leaf phase with no divergent branch: lanes
 // without a pending leaf, and the second record of a one-triangle leaf, load through a buffer
 // offset past the resource's range, which returns zeros without a memory access, and their tests
 // are masked off.  Straight-line code lets the closest-hit state stay in its registers (the
@@ -838,8 +650,7 @@ __device__ __forceinline__ float4 tri_unit(__amdgpu_buffer_rsrc_t rs, uint32_t o
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 }
 template <int FMT, typename Stack>
-__device__ __forceinline__ void leaf_step_flat(__amdgpu_buffer_rsrc_t trs, const float4* __restrict__ tbase, const Ray& r,
-                                               Trav& t, const Stack& stk) {
+__device__ __forceinline__ void leaf_step(__amdgpu_buffer_rsrc_t trs, const Ray& r, Trav& t, const Stack& stk) {
     const bool lf = t.node <= -2;
     const int v = ~t.node;
     const int unit = FMT == kFmtW4 ? (v >> 2) : 3 * (v >> 4);
@@ -867,7 +678,6 @@ __device__ __forceinline__ void leaf_step_flat(__amdgpu_buffer_rsrc_t trs, const
         t.sp = (lf & !more) ? max(sp - 1, 0) : sp;
     }
 }
-#endif
 
 // Highest VGPR the trace kernel claims, so that its allocation (granule 8) admits exactly
 // ARX_TRACE_WAVES waves per SIMD: 5 -> 88 VGPRs (512/88 = 5.8), 4 -> 104, 6 -> 80.  Every wave of
@@ -948,9 +758,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     }
     const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf) : (Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes));
     const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
-#if ARX_TRACE_LEAFFLAT
     const __amdgpu_buffer_rsrc_t trs = buffer_rsrc(tbase);
-#endif
     const uint64_t n = a.ray_end - a.ray_begin;
     const uint32_t wave_id = __builtin_amdgcn_readfirstlane(gid >> 6);
     const uint32_t n_waves = gridDim.x * (BLOCK / 64);
@@ -1102,19 +910,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                 ++pf[6];
                 pf[7] += __popcll(m_leaf);
 #endif
-#if ARX_TRACE_LEAFFLAT
 #if ARX_TRACE_COUNT
                 if (t.node <= -2) n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
 #endif
-                leaf_step_flat<FMT>(trs, tbase, r, t, stk);
-#else
-                if (t.node <= -2) {
-#if ARX_TRACE_COUNT
-                    n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
-#endif
-                    leaf_step<FMT>(tbase, r, t, stk);
-                }
-#endif
+                leaf_step<FMT>(trs, r, t, stk);
             }
         }
     }
@@ -1178,78 +977,6 @@ __global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float
     out[i] = make_float4(d.x, d.y, d.z, 0.0f);
 }
 
-#ifndef ARX_TRACE_SORT
-#define ARX_TRACE_SORT 0  // design experiment: rays in direction order (bits per octahedral axis; 0 off)
-#endif
-#if ARX_TRACE_SORT
-// Direction-ordered pre-pass (design experiment): the rays of a launch are counting-sorted by the
-// Morton code of their octahedral direction cell, so a wave's lanes start coherent.  A ray's id only
-// picks its direction and the int64 histogram is order-free, so the IR stays bit-identical.
-constexpr int kSortBits = ARX_TRACE_SORT;
-constexpr int kSortBins = 1 << (2 * kSortBits);
-__device__ __forceinline__ uint32_t dir_cell(float3 d) {
-    const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
-    float x = d.x / s, y = d.y / s;
-    if (d.z < 0.0f) {
-        const float ox = (1.0f - fabsf(y)) * (x >= 0.0f ? 1.0f : -1.0f);
-        const float oy = (1.0f - fabsf(x)) * (y >= 0.0f ? 1.0f : -1.0f);
-        x = ox;
-        y = oy;
-    }
-    const float m = (float)(1 << kSortBits);
-    const uint32_t u = (uint32_t)min(max((x * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
-    const uint32_t v = (uint32_t)min(max((y * 0.5f + 0.5f) * m, 0.0f), m - 1.0f);
-    uint32_t key = 0;
-#pragma unroll
-    for (int b = 0; b < kSortBits; ++b) key |= (((u >> b) & 1u) << (2 * b)) | (((v >> b) & 1u) << (2 * b + 1));
-    return key;
-}
-__global__ void dirs_count_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* tmp, uint32_t* bins,
-                                  unsigned long long* cursor) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *cursor = 0ull;
-    if (i >= count) return;
-    const float3 d = ray_direction(seed, first + i);
-    const uint32_t key = dir_cell(d);
-    tmp[i] = make_float4(d.x, d.y, d.z, __uint_as_float(key));
-    atomicAdd(bins + key, 1u);
-}
-// exclusive scan of kSortBins counts in place, one 1024-lane block
-__global__ void dirs_scan_kernel(uint32_t* bins) {
-    constexpr int per = (kSortBins + 1023) / 1024;
-    __shared__ uint32_t part[1024];
-    const int t = threadIdx.x;
-    uint32_t loc[per];
-    uint32_t sum = 0;
-    for (int k = 0; k < per; ++k) {
-        const int j = t * per + k;
-        loc[k] = j < kSortBins ? bins[j] : 0u;
-        sum += loc[k];
-    }
-    part[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
-    for (int k = 0; k < per; ++k) {
-        const int j = t * per + k;
-        if (j < kSortBins) bins[j] = run;
-        run += loc[k];
-    }
-}
-__global__ void dirs_scatter_kernel(const float4* __restrict__ tmp, float4* __restrict__ out, uint32_t* bins,
-                                    uint64_t count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const float4 v = tmp[i];
-    const uint32_t pos = atomicAdd(bins + __float_as_uint(v.w), 1u);
-    out[pos] = make_float4(v.x, v.y, v.z, 0.0f);
-}
-#endif
 
 __global__ void ray_dir_kernel(uint64_t seed, uint64_t first, uint64_t count, float* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1315,22 +1042,8 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     const bool dyn = n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
     a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
     a2.dyn_chunk = (uint32_t)kDynChunk;
-#if ARX_TRACE_SORT  // the dirs buffer holds 2 * n_rays float4 + kSortBins counters (arx_trace_rays)
-    {
-        float4* sorted = reinterpret_cast<float4*>(const_cast<void*>(args.dirs));
-        float4* tmp = sorted + n_rays;
-        uint32_t* bins = reinterpret_cast<uint32_t*>(tmp + n_rays);
-        (void)hipMemsetAsync(bins, 0, sizeof(uint32_t) * kSortBins, s);
-        const unsigned g = (unsigned)((n_rays + 255) / 256);
-        hipLaunchKernelGGL(dirs_count_kernel, dim3(g), dim3(256), 0, s, args.seed, args.ray_begin, n_rays, tmp, bins,
-                           args.cursor);
-        hipLaunchKernelGGL(dirs_scan_kernel, dim3(1), dim3(1024), 0, s, bins);
-        hipLaunchKernelGGL(dirs_scatter_kernel, dim3(g), dim3(256), 0, s, tmp, sorted, bins, n_rays);
-    }
-#else
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
                        args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
-#endif
     if (kSmallBlock > 0 && !dyn) {
         // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
