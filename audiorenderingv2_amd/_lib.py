@@ -130,6 +130,7 @@ SIGNATURES = {
     "arx_live_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_timing_ring": (C.c_int32, []),
     "arx_trace_kernel_id": (C.c_uint64, []),
+    "arx_debug_set_leaf_max": (C.c_int, [C.c_int32]),
     "arx_device_count": (C.c_int32, []),
     "arx_device_alloc": (C.c_int, [C.c_int32, C.c_size_t, C.POINTER(_P)]),
     "arx_device_free": (None, [C.c_int32, _P]),

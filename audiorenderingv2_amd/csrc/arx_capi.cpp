@@ -718,6 +718,12 @@ arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) 
 int32_t arx_timing_ring(void) { return arx_renderer::kTraceRing; }
 uint64_t arx_trace_kernel_id(void) { return trace_kernel_source_id(); }
 
+arx_status arx_debug_set_leaf_max(int32_t leaf_max) {
+    if (leaf_max < 1 || leaf_max > 15) return fail(ARX_ERR_INVALID_ARGUMENT, "leaf_max %d outside [1, 15]", leaf_max);
+    build_params().leaf_max = leaf_max;
+    return ARX_OK;
+}
+
 int32_t arx_device_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? (int32_t)n : -1;

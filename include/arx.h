@@ -305,6 +305,10 @@ arx_status arx_debug_scene_roundtrip(const float* tri_vertices, const float* tri
  * device re-quantizations issued so far into *requants. */
 arx_status arx_debug_node_images(arx_renderer* r, void* cnodes, void* qnodes, size_t n_nodes, float* grid,
                                  uint64_t* requants);
+/* Tests only: the most triangles the SAH builder may leave in one leaf (process-wide, for the
+ * builds that follow; production 2, range 1..15), so leaves of more than two triangles -- which
+ * production trees hold only below the builder's depth cap -- can be traced and checked. */
+arx_status arx_debug_set_leaf_max(int32_t leaf_max);
 /* Host only: build the scene, its 16-bit quantized BVH2 and its 4-wide compressed copy (CW4), and
  * trace n_rays random rays from the emitter through `bounces` specular reflections on the CPU with
  * both traversals (nearest first, f64 slab and triangle tests); out[16]: [0] queries, [1] / [2]

@@ -292,6 +292,34 @@ def test_random_soup_with_degenerate_triangles(path):
     assert_same_render(r, sc, (1.5, 1.2, -0.7), 0.0, (0.0, 0.0, 0.0), s)
 
 
+@pytest.mark.parametrize("path", PATHS)
+def test_leaves_of_more_than_two_triangles(path):
+    """Leaves of up to 8 triangles (builder leaf_max 8; production trees have them only below the
+    depth cap): the leaf step tests two triangles and continues with the same leaf two triangles on
+    (trace_kernel leaf_step), on every trace path.  Bit-exact with the oracle, whose tree differs."""
+    from audiorenderingv2_amd._lib import check, lib
+    from audiorenderingv2_amd.scene import _box_tris
+
+    rng = np.random.default_rng(23)
+    room = _box_tris(np.array([[-4, -4, -4]], np.float32), np.array([[4, 4, 4]], np.float32))
+    soup = rng.uniform(-3.5, 3.5, (2000, 9)).astype(np.float32)  # large, overlapping: leaves stay fat
+    tv = np.concatenate([room, soup]).astype(np.float32)
+    ta = rng.uniform(0.0, 0.9, tv.shape[0]).astype(np.float32)
+    sc = Scene(tv, ta, [])
+    s = RenderSettings(rays=(64, 64, 4), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
+    check(lib().arx_debug_set_leaf_max(8))
+    try:
+        r = make(sc, (1.5, 1.2, -0.7), emitter=(0.0, 0.0, 0.0), **s.__dict__)
+        r.set_trace_path(int(path))
+        assert_same_render(r, sc, (1.5, 1.2, -0.7), 0.0, (0.0, 0.0, 0.0), s)
+        cn = r.node_images()["cnodes"].view(np.int32).reshape(-1, 16)
+        codes = cn[:, 12:14].ravel()  # BvhNode d[0..1]: child codes
+        counts = (~codes[codes < -1]) & 15
+        assert counts.max() > 2, counts.max()
+    finally:
+        check(lib().arx_debug_set_leaf_max(2))
+
+
 @pytest.mark.parametrize("max_bounces,thres,secs", [(0, 0.0, 2), (1, 0.0, 1), (3, 0.05, 1), (64, 1e-7, 3)])
 def test_bounce_and_threshold_limits(c1_scene, max_bounces, thres, secs):
     """Reflection-count and energy-threshold cut-offs (devicePrograms.cu:147-175, 234-236)
