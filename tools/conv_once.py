@@ -19,6 +19,8 @@ if os.environ.get("ARX_LIB"):  # a design-experiment build (tools only)
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 x, sr = reference_audio("clapper")
+if os.environ.get("CONV_FRAMES"):  # a shorter signal (fewer block pairs), for the per-pair scaling
+    x = np.ascontiguousarray(x[:int(os.environ["CONV_FRAMES"])])
 r = AudioRenderer(RenderSettings(rays=(1, 1, 1), sample_rate=sr, ir_length_in_seconds=2))
 rng = np.random.default_rng(0)
 irs = []
@@ -34,6 +36,6 @@ for _ in range(n):
     r.convolute_device(dx.data_ptr(), x.size, dl.data_ptr(), dr.data_ptr())
     torch.cuda.synchronize()
     ms.append(r.conv_times(1)[0])
-print(f"conv {np.median(ms[1:] if n > 1 else ms) * 1e3:.1f} us (median of {max(n - 1, 1)}) "
+print(f"frames {x.size} conv {np.median(ms[1:] if n > 1 else ms) * 1e3:.1f} us (median of {max(n - 1, 1)}) "
       f"checksum {float(dl.double().abs().sum() + dr.double().abs().sum()):.9e} "
       f"lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}", flush=True)
