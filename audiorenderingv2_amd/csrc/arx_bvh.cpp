@@ -564,6 +564,160 @@ BvhNode make_node(const ChildRef& c0, const ChildRef& c1) {
     return n;
 }
 
+
+// ---- tree rotations (BuildParams::rotation_passes) ----
+namespace {
+float half_area(const ChildRef& c) {
+    const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+ChildRef node_child(const BvhNode& n, int s) {
+    ChildRef r;
+    const float* xy = s == 0 ? n.a : n.b;
+    r.lo[0] = xy[0];
+    r.hi[0] = xy[1];
+    r.lo[1] = xy[2];
+    r.hi[1] = xy[3];
+    r.lo[2] = n.c[2 * s];
+    r.hi[2] = n.c[2 * s + 1];
+    r.ref = n.d[s];
+    r.count = n.d[2 + s];
+    return r;
+}
+void set_node_child(BvhNode& n, int s, const ChildRef& r) {
+    float* xy = s == 0 ? n.a : n.b;
+    xy[0] = r.lo[0];
+    xy[1] = r.hi[0];
+    xy[2] = r.lo[1];
+    xy[3] = r.hi[1];
+    n.c[2 * s] = r.lo[2];
+    n.c[2 * s + 1] = r.hi[2];
+    n.d[s] = r.ref;
+    n.d[2 + s] = r.count;
+}
+bool is_inner(const ChildRef& c) { return c.count == 0 && c.ref >= 0; }
+ChildRef unite(const ChildRef& a, const ChildRef& b, int32_t ref) {
+    ChildRef r;
+    for (int k = 0; k < 3; ++k) {
+        r.lo[k] = std::min(a.lo[k], b.lo[k]);
+        r.hi[k] = std::max(a.hi[k], b.hi[k]);
+    }
+    r.ref = ref;
+    r.count = 0;
+    return r;
+}
+
+// Heights (1 + the children's, leaves 0) by a post-order walk from the root; returns the root's.
+int subtree_heights(const BvhBuild& b, std::vector<int>& h) {
+    h.assign(b.nodes.size(), 0);
+    if (!is_inner(b.root)) return 0;
+    std::vector<int32_t> order, st{b.root.ref};
+    while (!st.empty()) {
+        const int32_t v = st.back();
+        st.pop_back();
+        order.push_back(v);
+        for (int s = 0; s < 2; ++s) {
+            const ChildRef c = node_child(b.nodes[(size_t)v], s);
+            if (is_inner(c)) st.push_back(c.ref);
+        }
+    }
+    for (size_t k = order.size(); k-- > 0;) {
+        const int32_t v = order[k];
+        int m = 0;
+        for (int s = 0; s < 2; ++s) {
+            const ChildRef c = node_child(b.nodes[(size_t)v], s);
+            if (is_inner(c)) m = std::max(m, h[(size_t)c.ref]);
+        }
+        h[(size_t)v] = 1 + m;
+    }
+    return h[(size_t)b.root.ref];
+}
+
+// One top-down pass: at node N with children (L, R), L inner with children (L0, L1), swap R with
+// the Lx whose exchange gives the smallest new L' = (R, Ly), if that is smaller than L (only L's
+// box changes, so the sum of inner-node areas -- the SAH's traversal term -- drops by exactly the
+// difference).  R moves one level down: allowed only while R's deepest inner node stays within
+// the cap.  Boxes are unions of the stored (padded) child boxes, so every box stays conservative
+// and the leaves are untouched.  Returns the number of rotations.  (Kensler's grandchild <->
+// grandchild swaps as well: the same node visits per query on the C3 scene, not kept.)
+int64_t rotation_pass(BvhBuild& b, int cap) {
+    std::vector<int> h;
+    subtree_heights(b, h);
+    int64_t n_rot = 0;
+    std::vector<std::pair<int32_t, int>> q;  // (node, depth below the tree's root + 1)
+    if (is_inner(b.root)) q.push_back({b.root.ref, 1});
+    for (size_t qi = 0; qi < q.size(); ++qi) {
+        const int32_t N = q[qi].first;
+        const int dN = q[qi].second;
+        for (int side = 0; side < 2; ++side) {
+            const ChildRef L = node_child(b.nodes[(size_t)N], side), R = node_child(b.nodes[(size_t)N], 1 - side);
+            if (!is_inner(L) || (is_inner(R) && dN + 1 + h[(size_t)R.ref] > cap)) continue;
+            const float aL = half_area(L);
+            int best = -1;
+            float best_a = aL;
+            for (int x = 0; x < 2; ++x) {
+                const float a = half_area(unite(R, node_child(b.nodes[(size_t)L.ref], 1 - x), L.ref));
+                if (a < best_a) {
+                    best_a = a;
+                    best = x;
+                }
+            }
+            if (best < 0) continue;
+            const ChildRef Lx = node_child(b.nodes[(size_t)L.ref], best), Ly = node_child(b.nodes[(size_t)L.ref], 1 - best);
+            set_node_child(b.nodes[(size_t)L.ref], best, R);
+            set_node_child(b.nodes[(size_t)N], side, unite(R, Ly, L.ref));
+            set_node_child(b.nodes[(size_t)N], 1 - side, Lx);
+            h[(size_t)L.ref] = 1 + std::max(is_inner(R) ? h[(size_t)R.ref] : 0, is_inner(Ly) ? h[(size_t)Ly.ref] : 0);
+            ++n_rot;
+            break;  // one rotation per node and pass
+        }
+        for (int s = 0; s < 2; ++s) {
+            const ChildRef c = node_child(b.nodes[(size_t)N], s);
+            if (is_inner(c)) q.push_back({c.ref, dN + 1});
+        }
+    }
+    return n_rot;
+}
+}  // namespace
+
+void rotate_tree(BvhBuild& b, int passes) {
+    if (passes <= 0 || !is_inner(b.root)) return;
+    std::vector<int> h;
+    const int cap = subtree_heights(b, h);  // the deepest inner node stays where it was built
+    int64_t total = 0;
+    for (int p = 0; p < passes; ++p) {
+        const int64_t n = rotation_pass(b, cap);
+        total += n;
+        if (n == 0) break;
+    }
+    if (total == 0) return;
+    // Rotations move subtrees under other parents: renumber the nodes in depth-first pre-order
+    // (child 0 first, as the builder allocates them), so every parent precedes its children again
+    // (validate_bvh, bfs_prefix_order and the receiver refit's level schedule rely on it).
+    std::vector<int32_t> order, st{b.root.ref};
+    order.reserve(b.nodes.size());
+    while (!st.empty()) {
+        const int32_t v = st.back();
+        st.pop_back();
+        order.push_back(v);
+        for (int s = 1; s >= 0; --s) {
+            const ChildRef c = node_child(b.nodes[(size_t)v], s);
+            if (is_inner(c)) st.push_back(c.ref);
+        }
+    }
+    std::vector<int32_t> remap(b.nodes.size(), -1);
+    for (size_t k = 0; k < order.size(); ++k) remap[(size_t)order[k]] = (int32_t)k;
+    std::vector<BvhNode> out(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+        BvhNode nd = b.nodes[(size_t)order[k]];
+        for (int s = 0; s < 2; ++s)
+            if (nd.d[2 + s] == 0 && nd.d[s] >= 0) nd.d[s] = remap[(size_t)nd.d[s]];
+        out[k] = nd;
+    }
+    b.nodes.swap(out);
+    b.root.ref = remap[(size_t)b.root.ref];
+}
+
 void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, int64_t n, int32_t id_base,
                BvhBuild& out) {
     out.nodes.clear();
@@ -599,6 +753,7 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
         sb.refs_left = (int64_t)((double)sb.prm.spatial_budget * (double)n);
         out.tris.reserve((size_t)n + (size_t)sb.refs_left);
         out.root = sb.build(refs, 1);
+        rotate_tree(out, sb.prm.rotation_passes);
         return;
     }
     Builder b;

@@ -32,6 +32,9 @@ struct BvhBuild {
 #ifndef ARX_SAH_TRAV
 #define ARX_SAH_TRAV 1.0f
 #endif
+#ifndef ARX_BVH_ROTATIONS
+#define ARX_BVH_ROTATIONS 8
+#endif
 #ifndef ARX_SAH_LEAF_MAX
 #define ARX_SAH_LEAF_MAX 2
 #endif
@@ -66,6 +69,11 @@ struct BuildParams {
     // max_depth (the kernel's 28-entry LDS stack then needs no spill path).
     int max_depth = kLdsStack - 2;
     int threads = 8;  // top-level subtrees built concurrently (spatial builder)
+    // Tree rotations after the spatial build (Kensler 2008): passes over the tree, top down, each
+    // node swapping its smaller-area side's child with a grandchild when that shrinks the inner
+    // node between them, never deepening the tree past its built depth.  On the C3 scene: inner-
+    // node SAH -2.7 %, node visits per query -3.7 % (tools/bvh_stats.cpp).
+    int rotation_passes = ARX_BVH_ROTATIONS;
 };
 // Process-wide parameters: production defaults, never read from the environment; design tools
 // (tools/bvh_stats.cpp, tools/bvh_check.cpp) edit the struct before building.
@@ -77,6 +85,8 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 // Shift all node / triangle references by the given offsets (placing the build inside a
 // bigger array).  The root reference is shifted too.
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
+// Tree rotations on a finished build (BuildParams::rotation_passes; the spatial builder runs them).
+void rotate_tree(BvhBuild& b, int passes);
 // Renumber the nodes so the first k inner nodes in breadth-first order from the root take
 // indices 0..k-1 (the rest keep their order, so parents still precede their children): the
 // top levels of the scene tree share cache lines.

@@ -163,7 +163,9 @@ int main(int argc, char** argv) {
     if (const char* e = std::getenv("ALPHA")) bp.spatial_alpha = (float)std::atof(e);
     if (const char* e = std::getenv("SDEPTH")) bp.spatial_max_depth = std::atoi(e);
     if (const char* e = std::getenv("BUDGET")) bp.spatial_budget = (float)std::atof(e);
-    std::printf("params: bins %d leaf_max %d trav %.2f isect %.2f\n", bp.bins, bp.leaf_max, bp.trav_cost, bp.isect_cost);
+    if (const char* e = std::getenv("ROT")) bp.rotation_passes = std::atoi(e);
+    std::printf("params: bins %d leaf_max %d trav %.2f isect %.2f rotation passes %d\n", bp.bins, bp.leaf_max, bp.trav_cost,
+                bp.isect_cost, bp.rotation_passes);
     BvhBuild b;
     std::vector<float> ab(n, 0.5f);
     build_bvh(tv.data(), ab.data(), 0.5f, n, 0, b);
@@ -173,6 +175,12 @@ int main(int argc, char** argv) {
     std::printf("spatial %d alpha %g budget %g: refs %zu\n", (int)bp.spatial, bp.spatial_alpha, bp.spatial_budget, b.tris.size());
     std::printf("tris %ld  binary nodes %zu depth %d\n", n, b.nodes.size(), b.depth);
     t2.set_depths();
+    {
+        int md = 0;
+        for (size_t i = 0; i < t2.n; ++i)
+            if (t2.depth[i] < (1 << 20)) md = std::max(md, t2.depth[i]);
+        std::printf("max inner-node depth below the top node: %d\n", md);
+    }
     {
         long cnt[40] = {};
         for (size_t i = 0; i < t2.n; ++i) if (t2.depth[i] < 40) ++cnt[t2.depth[i]];
