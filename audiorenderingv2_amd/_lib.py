@@ -77,6 +77,10 @@ _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
 _I32 = C.POINTER(C.c_int32)
 
+# arx_debug_share_scene's transport callbacks (include/arx.h)
+SHARE_U64_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int)
+SHARE_BYTES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
+
 # name -> (restype, argtypes); must cover every function declared in include/arx.h
 SIGNATURES = {
     "arx_status_string": (C.c_char_p, [C.c_int]),
@@ -121,8 +125,6 @@ SIGNATURES = {
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
     "arx_debug_wide_stats": (C.c_int, [_F, _F, C.c_int64, _F, C.c_int64, C.c_int32, C.c_uint64, _D, C.c_size_t]),
-    "arx_debug_b16_stats": (C.c_int, [_F, _F, C.c_int64, _F, C.c_int64, C.c_int32, C.c_uint64, C.c_int32, _D,
-                                      C.c_size_t]),
     "arx_debug_trace_profile": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_debug_node_images": (C.c_int, [_P, _P, _P, C.c_size_t, _F, C.POINTER(C.c_uint64)]),
     "arx_trace_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -154,6 +156,9 @@ SIGNATURES = {
     "arx_group_ranks": (C.c_int32, [_P]),
     "arx_group_member": (_P, [_P, C.c_int32]),
     "arx_group_set_scene": (C.c_int, [_P, _F, _F, C.c_int64]),
+    "arx_group_shard": (None, [C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "arx_debug_share_scene": (C.c_int, [C.c_int32, _F, _F, C.c_int64, SHARE_U64_FN, SHARE_BYTES_FN, _P,
+                                        C.POINTER(C.c_uint64)]),
     "arx_group_set_receiver_model": (C.c_int, [_P, C.c_int, _F, C.c_int64]),
     "arx_group_set_emitter": (C.c_int, [_P, C.c_float, C.c_float, C.c_float]),
     "arx_group_set_listener": (C.c_int, [_P, C.c_float, C.c_float, C.c_float, C.c_float]),

@@ -26,8 +26,8 @@ LIB = os.path.join(PKG, "libarx.so")
 ARCH = os.environ.get("ARX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["arx_trace.hip", "arx_receiver.hip", "arx_conv.hip", "arx_capi.cpp", "arx_group.cpp", "arx_bvh.cpp", "arx_io.cpp",
-           "arx_wide.cpp", "arx_b16.cpp"]
-HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp", "arx_wide.hpp", "arx_b16.hpp"]
+           "arx_wide.cpp"]
+HEADERS = ["arx_layout.hpp", "arx_kernels.hpp", "arx_bvh.hpp", "arx_internal.hpp", "arx_wide.hpp", "arx_scene_share.hpp"]
 
 COMMON = [
     "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",

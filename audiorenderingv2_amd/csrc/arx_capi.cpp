@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <map>
 #include <mutex>
 #include <new>
@@ -176,8 +177,13 @@ arx_status prepare_receiver_model(arx_renderer* r) {
     std::vector<int32_t> lv(order);
     lv.insert(lv.end(), start.begin(), start.end());
     ARX_HIP(hipMemcpyAsync(r->d_recv_levels, lv.data(), lv.size() * sizeof(int32_t), hipMemcpyHostToDevice, r->stream));
-    // the receiver's CW4 layout (root at unit kW4RecvRoot, blocks after the scene's) for the refit
-    collapse_w4(r->recv, base, (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot, r->scene_img->w4.unit_end, r->recv4);
+    ARX_HIP(hipStreamSynchronize(r->stream));  // pageable sources
+    r->recv_level_count = (int32_t)order.size();
+    if (!r->use_w4) return ARX_OK;
+    // opt-in CW4 path only: the receiver's CW4 layout (root at unit kW4RecvRoot, blocks after the
+    // scene's) for the refit
+    collapse_w4(r->recv, base, (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot, r->scene_img->wide().w4.unit_end,
+                r->recv4);
     std::vector<int32_t> w4n(11 * r->recv4.nodes.size()), w4t(2 * r->recv4.leaf_tris.size());
     for (size_t i = 0; i < r->recv4.nodes.size(); ++i) {
         std::copy(r->recv4.src.begin() + 8 * i, r->recv4.src.begin() + 8 * i + 8, w4n.begin() + 11 * i);
@@ -201,7 +207,6 @@ arx_status prepare_receiver_model(arx_renderer* r) {
         ARX_HIP(hipMemcpyAsync(r->d_recv_w4_tris, w4t.data(), w4t.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));  // pageable sources
-    r->recv_level_count = (int32_t)order.size();
     return ARX_OK;
 }
 
@@ -230,6 +235,21 @@ void receiver_bound(const arx_renderer* r, float lo[3], float hi[3], bool* empty
     }
 }
 
+// The trace kernel addresses nodes and triangle records through buffer resources with 32-bit byte
+// offsets and num_records 0x7fffffff (arx_trace.hip buffer_rsrc; a load past it returns zeros, which
+// the leaf step uses for idle lanes): every record must end below 2^31 bytes, or a triangle would read
+// back as zeros (det 0, a silently dropped hit).  44.7 M triangle records / 33.5 M coded nodes.
+arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris) {
+    constexpr uint64_t kMax = 0x7fffffffull;
+    if ((uint64_t)n_tris * sizeof(TriRec) > kMax)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu triangle records x %zu B exceed the trace kernel's "
+                    "31-bit buffer offsets", (unsigned long long)n_tris, sizeof(TriRec));
+    if ((uint64_t)n_nodes * sizeof(BvhNode) > kMax)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu BVH nodes x %zu B exceed the trace kernel's "
+                    "31-bit buffer offsets", (unsigned long long)n_nodes, sizeof(BvhNode));
+    return ARX_OK;
+}
+
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_img) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
     const SceneImage& img = *r->scene_img;
@@ -255,11 +275,14 @@ arx_status ensure_device_scene(arx_renderer* r) {
         }
         build_bvh(tv.data(), ab.data(), 0.0f, (int64_t)ab.size(), (int32_t)img.n_input, r->recv);
         relocate_bvh(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size());
-        collapse_w4(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot,
-                    img.w4.unit_end, r->recv4);
+        if (r->use_w4)
+            collapse_w4(r->recv, 1 + (int32_t)sc.nodes.size(), (int32_t)sc.tris.size(), r->recv.root, kW4RecvRoot,
+                        img.wide().w4.unit_end, r->recv4);
     }
     const size_t n_nodes = 1 + sc.nodes.size() + r->recv.nodes.size();
     const size_t n_tris = sc.tris.size() + r->recv.tris.size();
+    arx_status fit = check_buffer_offsets(n_nodes, n_tris);
+    if (fit != ARX_OK) return fit;
     bool full = r->scene_dirty;
     if (n_nodes > r->nodes_cap) {
         if (r->d_cnodes) ARX_HIP(hipFree(r->d_cnodes));
@@ -280,11 +303,13 @@ arx_status ensure_device_scene(arx_renderer* r) {
         r->tris_cap = cap;
         full = true;
     }
-    // CW4: the buffer holds the scene's units, then the receiver's; the f32 records are the top node,
-    // the scene's nodes and (host-built receivers) the receiver's
-    const size_t w_units = std::max<size_t>(r->recv4.unit_end, img.w4.unit_end);
-    const size_t host_recv_w4 = r->recv_refit ? 0 : r->recv4.nodes.size();
-    const size_t n_w4f = 1 + img.w4.nodes.size() + host_recv_w4;
+    // CW4 (opt-in, use_w4 only): the buffer holds the scene's units, then the receiver's; the f32
+    // records are the top node, the scene's nodes and (host-built receivers) the receiver's
+    static const SceneImage::Wide kNoWide;
+    const SceneImage::Wide& wide = r->use_w4 ? img.wide() : kNoWide;
+    const size_t w_units = r->use_w4 ? std::max<size_t>(r->recv4.unit_end, wide.w4.unit_end) : 0;
+    const size_t host_recv_w4 = (r->recv_refit || !r->use_w4) ? 0 : r->recv4.nodes.size();
+    const size_t n_w4f = r->use_w4 ? 1 + wide.w4.nodes.size() + host_recv_w4 : 0;
     if (w_units > r->wbuf_cap) {
         if (r->d_wbuf) ARX_HIP(hipFree(r->d_wbuf));
         r->d_wbuf = nullptr;
@@ -362,46 +387,48 @@ arx_status ensure_device_scene(arx_renderer* r) {
         if (host_recv && !r->recv.tris.empty())
             ARX_HIP(hipMemcpyAsync(r->d_tris + sc.tris.size(), r->recv.tris.data(), r->recv.tris.size() * sizeof(TriRec),
                                    hipMemcpyHostToDevice, r->stream));
-        // CW4: the scene's buffer image and node records once per scene; the top node's record
-        // (child 0 the scene root, child 1 the host-built receiver's root or, on the refit path, a
-        // placeholder the refit kernel replaces); a host-built receiver's records and triangles
-        W4NodeF wtop;
-        std::memset(&wtop, 0, sizeof(wtop));
-        wtop.base = kW4SceneRoot;
-        wtop.self = 0;
-        if (sc.root.count >= 0) {
-            wtop.meta |= 1u;
-            for (int k = 0; k < 3; ++k) {
-                wtop.lo[0][k] = sc.root.lo[k];
-                wtop.hi[0][k] = sc.root.hi[k];
-            }
-        }
-        if (host_recv && r->recv.root.count >= 0) {
-            wtop.meta |= 1u << 2;
-            for (int k = 0; k < 3; ++k) {
-                wtop.lo[1][k] = r->recv.root.lo[k];
-                wtop.hi[1][k] = r->recv.root.hi[k];
-            }
-        }
-        ARX_HIP(hipMemcpyAsync(r->d_w4f, &wtop, sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
-        if (full && !img.wimage.empty())
-            ARX_HIP(hipMemcpyAsync(r->d_wbuf, img.wimage.data(), img.wimage.size() * sizeof(uint32_t),
-                                   hipMemcpyHostToDevice, r->stream));
-        if (full && !img.w4.nodes.empty())
-            ARX_HIP(hipMemcpyAsync(r->d_w4f + 1, img.w4.nodes.data(), img.w4.nodes.size() * sizeof(W4NodeF),
-                                   hipMemcpyHostToDevice, r->stream));
+        // CW4 (opt-in): the scene's buffer image and node records once per scene; the top node's
+        // record (child 0 the scene root, child 1 the host-built receiver's root or, on the refit
+        // path, a placeholder the refit kernel replaces); a host-built receiver's records and triangles
         std::vector<uint32_t> rimage;
-        if (host_recv) {
-            if (!r->recv4.nodes.empty())
-                ARX_HIP(hipMemcpyAsync(r->d_w4f + 1 + img.w4.nodes.size(), r->recv4.nodes.data(),
-                                       r->recv4.nodes.size() * sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
-            const size_t u0 = img.w4.unit_end;
-            rimage.assign((r->recv4.unit_end - u0) * 4, 0u);
-            for (const auto& lt : r->recv4.leaf_tris)
-                std::memcpy(rimage.data() + (size_t)(lt.first - u0) * 4, &r->recv.tris[(size_t)lt.second], sizeof(TriRec));
-            if (!rimage.empty())
-                ARX_HIP(hipMemcpyAsync(r->d_wbuf + u0, rimage.data(), rimage.size() * sizeof(uint32_t),
+        if (r->use_w4) {
+            W4NodeF wtop;
+            std::memset(&wtop, 0, sizeof(wtop));
+            wtop.base = kW4SceneRoot;
+            wtop.self = 0;
+            if (sc.root.count >= 0) {
+                wtop.meta |= 1u;
+                for (int k = 0; k < 3; ++k) {
+                    wtop.lo[0][k] = sc.root.lo[k];
+                    wtop.hi[0][k] = sc.root.hi[k];
+                }
+            }
+            if (host_recv && r->recv.root.count >= 0) {
+                wtop.meta |= 1u << 2;
+                for (int k = 0; k < 3; ++k) {
+                    wtop.lo[1][k] = r->recv.root.lo[k];
+                    wtop.hi[1][k] = r->recv.root.hi[k];
+                }
+            }
+            ARX_HIP(hipMemcpyAsync(r->d_w4f, &wtop, sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
+            if (full && !wide.wimage.empty())
+                ARX_HIP(hipMemcpyAsync(r->d_wbuf, wide.wimage.data(), wide.wimage.size() * sizeof(uint32_t),
                                        hipMemcpyHostToDevice, r->stream));
+            if (full && !wide.w4.nodes.empty())
+                ARX_HIP(hipMemcpyAsync(r->d_w4f + 1, wide.w4.nodes.data(), wide.w4.nodes.size() * sizeof(W4NodeF),
+                                       hipMemcpyHostToDevice, r->stream));
+            if (host_recv) {
+                if (!r->recv4.nodes.empty())
+                    ARX_HIP(hipMemcpyAsync(r->d_w4f + 1 + wide.w4.nodes.size(), r->recv4.nodes.data(),
+                                           r->recv4.nodes.size() * sizeof(W4NodeF), hipMemcpyHostToDevice, r->stream));
+                const size_t u0 = wide.w4.unit_end;
+                rimage.assign((r->recv4.unit_end - u0) * 4, 0u);
+                for (const auto& lt : r->recv4.leaf_tris)
+                    std::memcpy(rimage.data() + (size_t)(lt.first - u0) * 4, &r->recv.tris[(size_t)lt.second], sizeof(TriRec));
+                if (!rimage.empty())
+                    ARX_HIP(hipMemcpyAsync(r->d_wbuf + u0, rimage.data(), rimage.size() * sizeof(uint32_t),
+                                           hipMemcpyHostToDevice, r->stream));
+            }
         }
         ARX_HIP(hipStreamSynchronize(r->stream));
     }
@@ -412,8 +439,9 @@ arx_status ensure_device_scene(arx_renderer* r) {
         const size_t nq = host_recv ? n_nodes : 1 + sc.nodes.size();
         ARX_HIP(launch_requant16(r->d_cnodes, nq, r->qgrid, r->d_qnodes,
                                  reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
-        ARX_HIP(launch_requant_w4(r->d_w4f, r->n_w4f, r->qgrid, r->d_wbuf,
-                                  reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
+        if (r->use_w4)
+            ARX_HIP(launch_requant_w4(r->d_w4f, r->n_w4f, r->qgrid, r->d_wbuf,
+                                      reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
         ++r->requants;
     }
     r->q_valid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
@@ -440,7 +468,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
         a.cnodes = r->d_cnodes;
         a.qnodes = r->q_valid ? r->d_qnodes : nullptr;
         a.flag = reinterpret_cast<unsigned int*>(r->d_counters + 6);
-        if (r->q_valid) {  // the CW4 copy follows the quantized one (same grid)
+        if (r->q_valid && r->use_w4) {  // the opt-in CW4 copy follows the quantized one (same grid)
             a.wbuf = r->d_wbuf;
             a.w4_nodes = r->d_recv_w4;
             a.n_w4 = (int32_t)r->recv4.nodes.size();
@@ -462,7 +490,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
     r->stats.n_nodes = (int64_t)n_nodes;
     r->stats.bvh_depth = 1 + std::max(sc.depth, r->recv.depth);
     r->stats.tree_hash = img.hash;
-    r->depth4 = 1 + std::max(img.w4.depth, r->recv4.depth);
+    r->depth4 = r->use_w4 ? 1 + std::max(wide.w4.depth, r->recv4.depth) : 0;
     return ARX_OK;
 }
 
@@ -555,17 +583,23 @@ arx_status arx::check_scene_input(const float* tri_v, const float* tri_abs, int6
 }
 
 namespace {
-// The parts of a scene image derived from its BVH2: the coded copy, the CW4 collapse and the CW4
-// buffer's triangle image.
+// The part of a scene image derived from its BVH2: the coded copy.
 void finish_scene_image(SceneImage& img) {
     img.coded.resize(img.bvh.nodes.size());
     code_nodes(img.bvh.nodes.data(), img.bvh.nodes.size(), img.coded.data());
-    collapse_w4(img.bvh, 1, 0, img.bvh.root, kW4SceneRoot, kW4SceneUnit, img.w4);
-    img.wimage.assign((size_t)img.w4.unit_end * 4, 0u);
-    for (const auto& lt : img.w4.leaf_tris)
-        std::memcpy(img.wimage.data() + (size_t)lt.first * 4, &img.bvh.tris[(size_t)lt.second], sizeof(TriRec));
 }
 }  // namespace
+
+// The opt-in CW4 collapse and its buffer's triangle image, made once, on first request.
+const SceneImage::Wide& SceneImage::wide() const {
+    std::call_once(wide_once_, [this] {
+        collapse_w4(bvh, 1, 0, bvh.root, kW4SceneRoot, kW4SceneUnit, wide_.w4);
+        wide_.wimage.assign((size_t)wide_.w4.unit_end * 4, 0u);
+        for (const auto& lt : wide_.w4.leaf_tris)
+            std::memcpy(wide_.wimage.data() + (size_t)lt.first * 4, &bvh.tris[(size_t)lt.second], sizeof(TriRec));
+    });
+    return wide_;
+}
 
 namespace {
 // Process-wide cache of built scenes, keyed by a 128-bit hash of the input arrays: renderers and
@@ -575,10 +609,22 @@ std::mutex g_scene_cache_mu;
 std::map<std::pair<uint64_t, uint64_t>, std::weak_ptr<const SceneImage>> g_scene_cache;
 }  // namespace
 
+// The builder settings a tree depends on (build_params(): leaf size from arx_debug_set_leaf_max,
+// the tools' edits), hashed field by field so the scene cache never hands out a tree built with
+// other settings.  `threads` only changes the build's speed, not its result.
+uint64_t build_params_hash() {
+    const BuildParams& b = build_params();
+    const int32_t iv[] = {b.bins, b.leaf_max, b.spatial ? 1 : 0, b.spatial_bins, b.spatial_max_depth, b.max_depth,
+                          b.rotation_passes};
+    const float fv[] = {b.trav_cost, b.isect_cost, b.spatial_alpha, b.spatial_budget};
+    return hash_words(fv, sizeof(fv), hash_words(iv, sizeof(iv), 0xB7E151628AED2A6Bull));
+}
+
 SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_t n) {
     const size_t bytes = (size_t)(n > 0 ? n : 0);
+    const uint64_t prm = build_params_hash();
     const std::pair<uint64_t, uint64_t> key{
-        hash_words(tri_abs, bytes * sizeof(float), hash_words(tri_v, 9 * bytes * sizeof(float), 0x9E3779B97F4A7C15ull)),
+        hash_words(tri_abs, bytes * sizeof(float), hash_words(tri_v, 9 * bytes * sizeof(float), 0x9E3779B97F4A7C15ull)) ^ prm,
         hash_words(tri_v, 9 * bytes * sizeof(float), hash_words(tri_abs, bytes * sizeof(float), 0x6A09E667F3BCC909ull) ^
                                                          (uint64_t)n)};
     {
@@ -598,6 +644,8 @@ SceneRef arx::build_scene_image(const float* tri_v, const float* tri_abs, int64_
     img->hash = scene_hash(img->bvh);
     g_scene_builds.fetch_add(1);
     std::lock_guard<std::mutex> lock(g_scene_cache_mu);
+    for (auto it = g_scene_cache.begin(); it != g_scene_cache.end();)  // drop scenes nobody holds any more
+        it = it->second.expired() ? g_scene_cache.erase(it) : std::next(it);
     g_scene_cache[key] = img;
     return img;
 }
@@ -656,6 +704,8 @@ SceneRef arx::deserialize_scene(const uint8_t* p, size_t n, const char** why) {
 arx_status arx::set_scene_image(arx_renderer* r, SceneRef img) {
     const char* why = "";
     const BvhBuild& b = img->bvh;
+    const arx_status fit = check_buffer_offsets(1 + b.nodes.size(), b.tris.size());
+    if (fit != ARX_OK) return fit;
     if (!validate_bvh_range(b.nodes.data(), 1, b.nodes.size(), 1 + b.nodes.size(), b.tris.size(), &why))
         return fail(ARX_ERR_INTERNAL, "BVH validation failed (scene): %s", why);
     r->scene_img = std::move(img);
@@ -766,8 +816,9 @@ arx_status arx_debug_scene_roundtrip(const float* tri_v, const float* tri_abs, i
                       std::memcmp(a->bvh.nodes.data(), b->bvh.nodes.data(), a->bvh.nodes.size() * sizeof(BvhNode)) == 0 &&
                       std::memcmp(a->bvh.tris.data(), b->bvh.tris.data(), a->bvh.tris.size() * sizeof(TriRec)) == 0 &&
                       std::memcmp(a->coded.data(), b->coded.data(), a->coded.size() * sizeof(BvhNode)) == 0 &&
-                      a->wimage == b->wimage && a->w4.nodes.size() == b->w4.nodes.size() &&
-                      std::memcmp(a->w4.nodes.data(), b->w4.nodes.data(), a->w4.nodes.size() * sizeof(W4NodeF)) == 0 &&
+                      a->wide().wimage == b->wide().wimage && a->wide().w4.nodes.size() == b->wide().w4.nodes.size() &&
+                      std::memcmp(a->wide().w4.nodes.data(), b->wide().w4.nodes.data(),
+                                  a->wide().w4.nodes.size() * sizeof(W4NodeF)) == 0 &&
                       std::memcmp(&a->bvh.root, &b->bvh.root, sizeof(ChildRef)) == 0;
     if (!same) return fail(ARX_ERR_INTERNAL, "scene image round trip changed the tree");
     if (hash) *hash = a->hash;
@@ -866,11 +917,13 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
             return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     // the production trace kernels' register allocation, as the runtime sees it (arx_stats)
     for (int f = 0; f < 3; ++f)
-        if ((e = trace_kernel_occupancy(f, &r->occ[f][0], &r->occ[f][1], &r->occ[f][2])) != hipSuccess)
-            return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
-    r->stats.trace_vgprs = r->occ[kFmtQ16][0];
-    r->stats.trace_waves_per_simd = r->occ[kFmtQ16][1];
-    r->stats.trace_waves_target = r->occ[kFmtQ16][2];
+        for (int small = 0; small < 2; ++small)
+            if ((e = trace_kernel_occupancy(f, small != 0, &r->occ[f][small][0], &r->occ[f][small][1],
+                                            &r->occ[f][small][2])) != hipSuccess)
+                return cleanup(fail(ARX_ERR_HIP, "arx_create: trace kernel attributes: %s", hipGetErrorString(e)));
+    r->stats.trace_vgprs = r->occ[kFmtQ16][0][0];
+    r->stats.trace_waves_per_simd = r->occ[kFmtQ16][0][1];
+    r->stats.trace_waves_target = r->occ[kFmtQ16][0][2];
     r->stats.trace_format = kFmtQ16;
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
@@ -1104,10 +1157,12 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
 #endif
     const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
     const int fmt = a.wbuf ? kFmtW4 : (a.qnodes ? kFmtQ16 : kFmtF32);
+    // the instance launch_trace takes (ray pool or small launch): the profile guard reads these
+    const int small = trace_uses_small_block(a, r->cus, r->force_global_stack) ? 1 : 0;
     r->stats.trace_format = fmt;
-    r->stats.trace_vgprs = r->occ[fmt][0];
-    r->stats.trace_waves_per_simd = r->occ[fmt][1];
-    r->stats.trace_waves_target = r->occ[fmt][2];
+    r->stats.trace_vgprs = r->occ[fmt][small][0];
+    r->stats.trace_waves_per_simd = r->occ[fmt][small][1];
+    r->stats.trace_waves_target = r->occ[fmt][small][2];
     ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
@@ -1411,7 +1466,12 @@ arx_status arx_debug_set_trace_path(arx_renderer* r, int path) {
     if (!r || path < 0 || path > 15 || (path & 4)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
     r->force_f32_nodes = (path & 1) != 0;
     r->force_global_stack = (path & 2) != 0;
-    r->use_w4 = (path & 8) != 0;
+    const bool w4 = (path & 8) != 0;
+    if (w4 && !r->use_w4) {  // the opt-in CW4 copy is made and uploaded at the next trace
+        r->scene_dirty = true;
+        r->recv_model_dirty = true;
+    }
+    r->use_w4 = w4;
     return ARX_OK;
 }
 

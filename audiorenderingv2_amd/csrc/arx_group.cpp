@@ -23,9 +23,11 @@
 #include <cmath>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "arx_internal.hpp"
+#include "arx_scene_share.hpp"
 
 using namespace arx;
 
@@ -200,61 +202,157 @@ arx_renderer* arx_group_member(arx_group* g, int32_t i) {
 // The scene tree is built once per group (buildAccel, AudioRenderer.cpp:95-218, runs once per scene
 // in the reference too) and shared by the members; each uploads it to its own device at its next
 // trace.  In a one-GPU-per-process group, rank 0 builds and the tree's byte image goes to the other
-// ranks with one RCCL broadcast (staged through device memory on the member's stream).
+// ranks with RCCL broadcasts (share_from_rank0, arx_scene_share.hpp: every rank enters every
+// collective, a failure on any rank fails the call on all of them).
+}  // extern "C"
+
+namespace {
+// share_from_rank0's transport over the group's communicator, staged through device memory on the
+// member's stream.
+struct RcclChannel {
+    ncclComm_t comm;
+    hipStream_t stream;
+    bool root;
+    uint64_t* d_word = nullptr;
+    uint8_t* d_buf = nullptr;
+    std::string err;
+
+    ~RcclChannel() {
+        hipStreamSynchronize(stream);
+        hipFree(d_word);
+        hipFree(d_buf);
+    }
+    bool hip(hipError_t e, const char* what) {
+        if (e != hipSuccess && err.empty()) err = std::string(what) + ": " + hipGetErrorString(e);
+        return e == hipSuccess;
+    }
+    bool nccl(ncclResult_t e, const char* what) {
+        if (e != ncclSuccess && err.empty()) err = std::string(what) + ": " + ncclGetErrorString(e);
+        return e == ncclSuccess;
+    }
+    bool word(uint64_t* v, bool bcast) {
+        if (!d_word && !hip(hipMalloc(&d_word, sizeof(uint64_t)), "hipMalloc")) return false;
+        return hip(hipMemcpyAsync(d_word, v, sizeof(uint64_t), hipMemcpyHostToDevice, stream), "upload") &&
+               nccl(bcast ? ncclBroadcast(d_word, d_word, 1, ncclUint64, 0, comm, stream)
+                          : ncclAllReduce(d_word, d_word, 1, ncclUint64, ncclMax, comm, stream),
+                    bcast ? "ncclBroadcast(size)" : "ncclAllReduce(flag)") &&
+               hip(hipMemcpyAsync(v, d_word, sizeof(uint64_t), hipMemcpyDeviceToHost, stream), "download") &&
+               hip(hipStreamSynchronize(stream), "sync");
+    }
+    bool bcast_u64(uint64_t* v) { return word(v, true); }
+    bool max_u64(uint64_t* v) { return word(v, false); }
+    bool stage(uint64_t bytes) { return hip(hipMalloc(&d_buf, std::max<uint64_t>(bytes, 1)), "hipMalloc(image)"); }
+    bool bcast_bytes(uint8_t* host, uint64_t bytes) {
+        return (!root || hip(hipMemcpyAsync(d_buf, host, bytes, hipMemcpyHostToDevice, stream), "upload")) &&
+               nccl(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, 0, comm, stream), "ncclBroadcast(tree)") &&
+               (root || hip(hipMemcpyAsync(host, d_buf, bytes, hipMemcpyDeviceToHost, stream), "download")) &&
+               hip(hipStreamSynchronize(stream), "sync");
+    }
+};
+
+// share_from_rank0's transport through caller callbacks (arx_debug_share_scene).
+struct CallbackChannel {
+    arx_share_u64_fn word;
+    arx_share_bytes_fn bytes_fn;
+    void* ctx;
+    std::string err;
+    bool bcast_u64(uint64_t* v) { return word(ctx, v, 0) == 0 || (err = "word broadcast failed", false); }
+    bool max_u64(uint64_t* v) { return word(ctx, v, 1) == 0 || (err = "word all-reduce failed", false); }
+    bool stage(uint64_t) { return true; }
+    bool bcast_bytes(uint8_t* host, uint64_t n) { return bytes_fn(ctx, host, n) == 0 || (err = "byte broadcast failed", false); }
+};
+
+// arx_group_set_scene's rank path over any transport: rank 0 checks and builds the scene, every other
+// rank reads the broadcast image; every rank returns the same status class.
+template <class Chan>
+arx_status share_scene(Chan& ch, int32_t rank, const float* tri_v, const float* tri_abs, int64_t n, SceneRef* out) {
+    SceneRef img;
+    arx_status root_st = ARX_OK;
+    std::string root_err, consume_err;
+    const ShareResult res = share_from_rank0(
+        ch, rank,
+        [&](std::vector<uint8_t>& bytes) {
+            root_st = check_scene_input(tri_v, tri_abs, n);
+            if (root_st == ARX_OK) {
+                img = build_scene_image(tri_v, tri_abs, n);
+                if (!img) root_st = fail(ARX_ERR_OUT_OF_MEMORY, "scene build failed");
+            }
+            if (root_st != ARX_OK) {
+                root_err = arx_last_error();
+                return false;
+            }
+            bytes = serialize_scene(*img);
+            return true;
+        },
+        [&](const std::vector<uint8_t>& bytes) {
+            const char* why = "";
+            img = deserialize_scene(bytes.data(), bytes.size(), &why);
+            if (!img) consume_err = why;
+            return (bool)img;
+        });
+    switch (res) {
+        case ShareResult::ok:
+            *out = img;
+            return ARX_OK;
+        case ShareResult::root_failed:
+            return rank == 0 ? fail(root_st, "%s", root_err.c_str())
+                             : fail(ARX_ERR_INVALID_ARGUMENT, "scene broadcast: rank 0 could not build the scene");
+        case ShareResult::staging_failed:
+            return fail(ARX_ERR_OUT_OF_MEMORY, "scene broadcast (rank %d): a rank could not stage the image%s%s", rank,
+                        ch.err.empty() ? "" : ": ", ch.err.c_str());
+        case ShareResult::consume_failed:
+            return fail(ARX_ERR_INTERNAL, "scene broadcast (rank %d): a rank could not read the image%s%s", rank,
+                        consume_err.empty() ? "" : ": ", consume_err.c_str());
+        case ShareResult::transport_failed:
+            break;
+    }
+    return fail(ARX_ERR_HIP, "scene broadcast (rank %d): %s", rank, ch.err.c_str());
+}
+
+// Rank r of G traces the global ray ids [r*N/G, (r+1)*N/G) of the N-ray launch.
+void shard_of(uint64_t n, int32_t rank, int32_t n_ranks, uint64_t* b, uint64_t* e) {
+    const unsigned __int128 nn = n;
+    *b = (uint64_t)(nn * (uint64_t)rank / (uint64_t)n_ranks);
+    *e = (uint64_t)(nn * (uint64_t)(rank + 1) / (uint64_t)n_ranks);
+}
+}  // namespace
+
+extern "C" {
+
 arx_status arx_group_set_scene(arx_group* g, const float* tri_v, const float* tri_abs, int64_t n) {
     if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
     const bool rank_path = g->n_ranks > 1 && g->members.size() == 1 && g->comms.size() == 1;
     SceneRef img;
-    if (!rank_path || g->rank0 == 0) {
+    if (!rank_path) {
         const arx_status st = check_scene_input(tri_v, tri_abs, n);
         if (st != ARX_OK) return st;
         img = build_scene_image(tri_v, tri_abs, n);
         if (!img) return fail(ARX_ERR_OUT_OF_MEMORY, "scene build failed");
-    }
-    if (rank_path) {
+    } else {
         arx_renderer* r = g->members[0];
         ARX_HIP(hipSetDevice(r->cfg.device));
-        std::vector<uint8_t> bytes;
-        uint64_t size = 0;
-        if (g->rank0 == 0) {
-            bytes = serialize_scene(*img);
-            size = bytes.size();
-        }
-        uint64_t* d_size = nullptr;
-        uint8_t* d_buf = nullptr;
-        auto release = [&]() {
-            hipStreamSynchronize(r->stream);
-            hipFree(d_size);
-            hipFree(d_buf);
-        };
-        arx_status st = ARX_OK;
-        auto step = [&](hipError_t e, const char* what) {
-            if (st == ARX_OK && e != hipSuccess) st = fail(ARX_ERR_HIP, "scene broadcast: %s: %s", what, hipGetErrorString(e));
-        };
-        auto nstep = [&](ncclResult_t e, const char* what) {
-            if (st == ARX_OK && e != ncclSuccess) st = fail(ARX_ERR_HIP, "scene broadcast: %s: %s", what, ncclGetErrorString(e));
-        };
-        step(hipMalloc(&d_size, sizeof(uint64_t)), "hipMalloc");
-        step(hipMemcpyAsync(d_size, &size, sizeof(uint64_t), hipMemcpyHostToDevice, r->stream), "size upload");
-        nstep(ncclBroadcast(d_size, d_size, 1, ncclUint64, 0, g->comms[0], r->stream), "size");
-        step(hipMemcpyAsync(&size, d_size, sizeof(uint64_t), hipMemcpyDeviceToHost, r->stream), "size download");
-        step(hipStreamSynchronize(r->stream), "sync");
-        if (st == ARX_OK && g->rank0 != 0) bytes.resize(size);
-        step(hipMalloc(&d_buf, std::max<uint64_t>(size, 1)), "hipMalloc");
-        if (g->rank0 == 0) step(hipMemcpyAsync(d_buf, bytes.data(), size, hipMemcpyHostToDevice, r->stream), "upload");
-        nstep(ncclBroadcast(d_buf, d_buf, size, ncclUint8, 0, g->comms[0], r->stream), "tree");
-        if (g->rank0 != 0) step(hipMemcpyAsync(bytes.data(), d_buf, size, hipMemcpyDeviceToHost, r->stream), "download");
-        step(hipStreamSynchronize(r->stream), "sync");
-        release();
+        RcclChannel ch{g->comms[0], r->stream, g->rank0 == 0};
+        const arx_status st = share_scene(ch, g->rank0, tri_v, tri_abs, n, &img);
         if (st != ARX_OK) return st;
-        if (g->rank0 != 0) {
-            const char* why = "";
-            img = deserialize_scene(bytes.data(), bytes.size(), &why);
-            if (!img) return fail(ARX_ERR_INTERNAL, "scene broadcast: %s", why);
-        }
     }
-    return for_all(g, [&](arx_renderer* r) { return set_scene_image(r, img); });
+    return for_all(g, [&](arx_renderer* m) { return set_scene_image(m, img); });
 }
+
+void arx_group_shard(uint64_t n_rays, int32_t rank, int32_t n_ranks, uint64_t* begin, uint64_t* end) {
+    shard_of(n_rays, rank, n_ranks, begin, end);
+}
+
+// The rank path's scene hand-over over a caller's transport (tests: two processes over gloo).
+arx_status arx_debug_share_scene(int32_t rank, const float* tri_v, const float* tri_abs, int64_t n,
+                                 arx_share_u64_fn word, arx_share_bytes_fn bytes, void* ctx, uint64_t* tree_hash) {
+    if (rank < 0 || !word || !bytes) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    CallbackChannel ch{word, bytes, ctx};
+    SceneRef img;
+    const arx_status st = share_scene(ch, rank, tri_v, tri_abs, n, &img);
+    if (st == ARX_OK && tree_hash) *tree_hash = img->hash;
+    return st;
+}
+
 arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_v, int64_t n) {
     return for_all(g, [&](arx_renderer* r) { return arx_set_receiver_model(r, side, tri_v, n); });
 }
@@ -287,9 +385,10 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
     // 1. every local member traces its shard (async on its own stream)
     for (size_t i = 0; i < g->members.size(); ++i) {
         arx_renderer* r = g->members[i];
-        const uint64_t rank = (uint64_t)g->rank0 + i;
+        uint64_t b = 0, e = 0;
+        shard_of(n, g->rank0 + (int32_t)i, g->n_ranks, &b, &e);
         arx_status st = arx_clear_histogram(r);
-        if (st == ARX_OK) st = arx_trace_rays(r, n * rank / (uint64_t)g->n_ranks, n * (rank + 1) / (uint64_t)g->n_ranks);
+        if (st == ARX_OK) st = arx_trace_rays(r, b, e);
         if (st != ARX_OK) return st;
     }
     // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:

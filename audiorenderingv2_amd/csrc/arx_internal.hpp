@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -48,11 +49,19 @@ inline uint64_t n_rays(const arx_config& c) {
 struct SceneImage {
     BvhBuild bvh;
     std::vector<BvhNode> coded;
-    W4Build w4;                  // the CW4 copy: scene root at unit 2, blocks from unit kW4SceneUnit
-    std::vector<uint32_t> wimage;  // CW4 buffer units [0, w4.unit_end) x 4 words: leaf triangles
-                                   // filled, node slots zero (quantized on the device)
     int64_t n_input = 0;  // triangles given to arx_set_scene (global ids 0 .. n_input-1)
     uint64_t hash = 0;    // content hash of nodes and triangle records (profile guards)
+    // The opt-in 4-wide compressed copy (CW4, arx_debug_set_trace_path bit 3; measured 1.9x slower
+    // than the BVH2): made on first request only, never by the product path.
+    struct Wide {
+        W4Build w4;                    // scene root at unit 2, blocks from unit kW4SceneUnit
+        std::vector<uint32_t> wimage;  // CW4 buffer units [0, w4.unit_end) x 4 words: leaf triangles
+                                       // filled, node slots zero (quantized on the device)
+    };
+    const Wide& wide() const;
+  private:
+    mutable std::once_flag wide_once_;
+    mutable Wide wide_;
 };
 // CW4 buffer: top node at unit 0, its block (scene root node, receiver root node) at units 2..5
 constexpr uint32_t kW4SceneRoot = 2, kW4RecvRoot = 4, kW4SceneUnit = 6;
@@ -131,7 +140,7 @@ struct arx_renderer {
     int32_t* d_recv_w4_tris = nullptr;
     bool use_w4 = false;           // arx_debug_set_trace_path bit 3: the CW4 tree
     int32_t depth4 = 0;            // CW4 levels (top node included): bounds the stack (3 per level)
-    int32_t occ[3][3] = {};        // per node format: VGPRs, waves admitted, waves targeted
+    int32_t occ[3][2][3] = {};     // per node format and instance (0 pool, 1 small launches): VGPRs, waves admitted, waves targeted
     arx::QGrid qgrid{};
     bool qgrid_set = false;
     bool q_valid = false;         // d_qnodes matches the tree (re-quantized on the device, arx_receiver.hip)

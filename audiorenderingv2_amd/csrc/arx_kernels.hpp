@@ -25,7 +25,10 @@ hipError_t launch_clear(unsigned long long* hist, uint64_t n, unsigned long long
 hipError_t launch_ray_directions(uint64_t seed, uint64_t first, uint64_t count, float* d_out, hipStream_t s);
 // Register allocation of the production trace kernel instance (hipFuncGetAttributes numRegs), the
 // waves per SIMD it admits, and the waves per SIMD the persistent grid is sized for.
-hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target);
+// Register allocation of the LDS-stack trace instance of node format fmt, the large-launch (ray pool)
+// or the small-launch one (small), and which of the two launch_trace takes for these arguments.
+hipError_t trace_kernel_occupancy(int fmt, bool small, int* vgprs, int* waves_admitted, int* waves_target);
+bool trace_uses_small_block(const TraceArgs& a, int cus, bool force_global_stack);
 // identity of the trace kernel in this build (build.py trace_source_id; arx_trace_kernel_id)
 uint64_t trace_kernel_source_id();
 

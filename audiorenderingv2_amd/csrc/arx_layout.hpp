@@ -87,23 +87,6 @@ struct alignas(16) W4NodeF {
 };
 static_assert(sizeof(W4NodeF) == 112, "W4NodeF must be 112 B");
 
-// ---- compact binary tree (B16, arx_b16.hpp) ----------------------------------------------------
-// The BVH2 with one 16-B unit per node, in a buffer of 16-B units shared with the triangle records
-// (as CW4's):
-//   w0, w1, w2 = x, y, z planes as bytes (c0 lo, c0 hi, c1 lo, c1 hi) on the node's block frame
-//   w3 = kind0 | kind1 << 4 | base << 8: kind 0 empty, kB16Inner inner node, 1..14 a leaf of that
-//        many triangles; the children chunk at `base` holds the inner children (one unit each, in
-//        child order), then the leaves' TriRecs (3 units each, in child order)
-// Frame of block b (units [b << kB16BlockBits, (b + 1) << kB16BlockBits)): uint2 (ox | oy << 16,
-// oz | ex << 16 | ey << 20 | ez << 24): plane q of axis k is 16-bit grid quantum o_k + q * 2^e_k.
-// Unit 0 is the top node, unit 1 the scene root, unit 2 the receiver root (block 0).
-#ifndef ARX_B16_BLOCK_BITS
-#define ARX_B16_BLOCK_BITS 6  // design experiments only (build.py --exp)
-#endif
-constexpr int kB16BlockBits = ARX_B16_BLOCK_BITS;
-constexpr uint32_t kB16Inner = 15u;
-constexpr uint32_t kB16SceneRoot = 1u, kB16RecvRoot = 2u;
-
 // Stack-entry / child code of an empty child in the coded and quantized nodes (code_nodes,
 // arx_bvh.hpp): a leaf of 0 triangles (-1 is kept free: it means "no entry").
 constexpr int32_t kEmptyChildCode = ~16;

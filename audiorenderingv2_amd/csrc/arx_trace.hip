@@ -1029,6 +1029,15 @@ int trace_grid(const TraceArgs& args, int cus, uint64_t n_rays) {
     return (int)std::max<uint64_t>(1, std::min(want, cap));
 }
 
+// The ray pool (and the kBlock instance) for launches with at least kDynMinRaysPerWave rays per wave
+// of the full grid; smaller launches take the kSmallBlock instance with static ranges.
+template <int FMT, bool GSTACK>
+bool uses_pool(const TraceArgs& args, int cus) {
+    const uint64_t n_rays = args.ray_end - args.ray_begin;
+    const int grid = trace_grid<kBlock, GSTACK, FMT>(args, cus, n_rays);
+    return n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
+}
+
 template <int FMT, bool GSTACK>
 hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     const uint64_t n_rays = args.ray_end - args.ray_begin;
@@ -1039,7 +1048,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
 #endif
     const int grid = trace_grid<kBlock, GSTACK, FMT>(args, cus, n_rays);
     TraceArgs a2 = args;
-    const bool dyn = n_rays >= (uint64_t)kDynMinRaysPerWave * (uint64_t)grid * (kBlock / 64);
+    const bool dyn = uses_pool<FMT, GSTACK>(args, cus);
     a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
     a2.dyn_chunk = (uint32_t)kDynChunk;
     hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
@@ -1079,13 +1088,28 @@ hipError_t launch_trace(const TraceArgs& a, int cus, hipStream_t s, bool force_g
 #endif
 uint64_t trace_kernel_source_id() { return ARX_TRACE_SRC_ID; }
 
-hipError_t trace_kernel_occupancy(int fmt, int* vgprs, int* waves_admitted, int* waves_target) {
+bool trace_uses_small_block(const TraceArgs& a, int cus, bool force_global_stack) {
+    if (kSmallBlock <= 0 || a.ray_end <= a.ray_begin) return false;
+    if (a.wbuf) return !uses_pool<kFmtW4, false>(a, cus);
+    const bool gstack = force_global_stack || a.bvh_depth + 1 > kLdsStack;
+    if (a.qnodes) return gstack ? !uses_pool<kFmtQ16, true>(a, cus) : !uses_pool<kFmtQ16, false>(a, cus);
+    return gstack ? !uses_pool<kFmtF32, true>(a, cus) : !uses_pool<kFmtF32, false>(a, cus);
+}
+
+namespace {
+template <int B, int L, int S>
+const void* lds_stack_instance(int fmt) {
+    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtW4, false>)
+           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtQ16, false>)
+                            : reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtF32, false>);
+}
+}  // namespace
+
+hipError_t trace_kernel_occupancy(int fmt, bool small, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;
-    const void* k =
-        fmt == kFmtW4 ? reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtW4, false>)
-        : fmt == kFmtQ16
-            ? reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtQ16, false>)
-            : reinterpret_cast<const void*>(trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, kFmtF32, false>);
+    constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
+    const void* k = small ? lds_stack_instance<SB, kSmallLeaf, kSmallSteps>(fmt)
+                          : lds_stack_instance<kBlock, kLeafThresh, kSteps>(fmt);
     const hipError_t e = hipFuncGetAttributes(&fa, k);
     if (e != hipSuccess) return e;
     // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8

@@ -230,8 +230,12 @@ def _cpu_model() -> str:
 
 
 # ------------------------------------------------------------------------------- extra legs ---
+C5 = dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000)  # configs[4]: 1M rays x 16 per frame in total
+
+
 def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int) -> dict:
-    """the listener moves 0.05 m/frame along +x with yaw += 1 deg/frame.
+    """SURVEY.md §8d C5 (configs[4]): 1M rays x 16 bounces per frame in total, sharded over the job's
+    GPUs (125K per GPU on 8), the listener moving 0.05 m/frame along +x with yaw += 1 deg/frame.
     Frame latency = host wall time of: receiver re-placement (receiver sub-tree only, no scene
     rebuild; a grid that grows is re-quantized on the device) -> trace every GPU's shard -> RCCL
     all-reduce -> finalize IR -> new IR spectra for the file and the live convolution paths on every
@@ -253,10 +257,21 @@ def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int) -> dict:
         if k >= 3:  # first frames warm the receiver rebuild path
             lat.append((time.perf_counter() - t0) * 1e3)
     a = np.array(lat)
-    return {"frames": frames, "rays_per_gpu": rays_per_gpu, "p50_ms": ranks.max(float(np.percentile(a, 50))),
+    return {"frames": frames, "rays_per_frame": int(np.prod(C5["rays"])), "rays_per_gpu": rays_per_gpu,
+            "gpus": g.n_ranks, "p50_ms": ranks.max(float(np.percentile(a, 50))),
             "p99_ms": ranks.max(float(np.percentile(a, 99))), "max_ms": ranks.max(float(a.max())),
             "budget_ms": 1000.0 / 60.0, "walk_m": 0.05 * (frames + 2),
-            "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + all-reduce + finalize + IR spectra"}
+            "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + RCCL all-reduce (N > 1) + finalize + "
+                         "IR spectra, on a C5 group of its own (1M rays x 16 per frame over all GPUs)"}
+
+
+def allreduce_model_us(n_ranks: int, nbytes: int, alpha_us: float = 3.0, link_gbs: float = 153.0) -> float:
+    """Ring all-reduce over xGMI: 2 (G - 1) dependent steps of latency alpha plus 2 (G - 1) / G of the
+    buffer through one link (ring collectives are per-link bound; one xGMI link ~153 GB/s).  A model
+    for the one-GPU box; on an N-GPU node the moving-listener leg measures the real one."""
+    if n_ranks <= 1:
+        return 0.0
+    return 2 * (n_ranks - 1) * alpha_us + 2 * (n_ranks - 1) / n_ranks * nbytes / (link_gbs * 1e9) * 1e6
 
 
 def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: int) -> dict:
@@ -280,12 +295,18 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
         r.stats()  # synchronises the renderer's stream
         if k >= 3:
             lat.append((time.perf_counter() - t0) * 1e3)
+    hist_bytes = 2 * r.ir_length * 8  # the int64 histogram the 8 ranks all-reduce
     r.close()
     a = np.array(lat)
+    ar_ms = allreduce_model_us(8, hist_bytes) / 1e3
     return {"frames": frames, "rays_per_gpu": shard, "p50_ms": float(np.percentile(a, 50)),
             "p99_ms": float(np.percentile(a, 99)), "max_ms": float(a.max()), "budget_ms": 1000.0 / 60.0,
+            "allreduce_model_ms": ar_ms, "p50_ms_with_allreduce": float(np.percentile(a, 50)) + ar_ms,
+            "max_ms_with_allreduce": float(a.max()) + ar_ms,
+            "allreduce_model": f"ring over 8 GPUs, {hist_bytes} B int64 histogram: 14 steps x 3 us + 1.75 x bytes "
+                               "at 153 GB/s (one xGMI link); the 8-GPU run's moving_listener measures it",
             "per_frame": "one GPU's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra "
-                         "(projected 8-GPU rank; the all-reduce is not included)"}
+                         "(projected 8-GPU rank) + the modelled all-reduce"}
 
 
 def pipelined_leg(groups, bufs, frames: int, steps: int, warmup: int, ranks: "Ranks", one_frame_ms: float) -> dict:
@@ -448,10 +469,10 @@ def main(argv=None) -> int:
     t_setup = time.perf_counter()
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
         if plan["mode"] == "rank":
-            uids = share_unique_ids(rank, world, os.environ, RenderGroup.unique_id, 2)
+            uids = share_unique_ids(rank, world, os.environ, RenderGroup.unique_id, 3)
             g = RenderGroup.rank(settings, world, rank, uids[0], scene=scene, receiver=receiver)
         else:
-            uids = [None, None]
+            uids = [None, None, None]
             g = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
     ranks = Ranks(g, plan["mode"])
     ranks.barrier()
@@ -514,8 +535,7 @@ def main(argv=None) -> int:
 
     value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
-    # frames in flight, before the moving-listener leg: that leg's walk grows the quantization grid
-    # of g for good (the grid only grows), which a fresh second group would not share
+    # frames in flight: a second group beside g
     pipelined = None
     if not args.no_pipelined:
         with _stdout_to_stderr():
@@ -533,7 +553,18 @@ def main(argv=None) -> int:
             for x in b:
                 x.close()
         g2.close()
-    moving = moving_listener(g, ranks, args.c5_frames, total_rays // world) if args.c5_frames > 0 else None
+    moving = None
+    if args.c5_frames > 0:  # C5 on a group of its own: 1M rays per frame in total, sharded over the GPUs
+        s5 = RenderSettings(rays=C5["rays"], ir_length_in_seconds=2, sample_rate=C5["sample_rate"], base_power=3.62,
+                            max_bounces=C5["max_bounces"], hrtf_absorption_rate=1.0, seed=1, device=plan["devices"][0])
+        with _stdout_to_stderr():
+            if plan["mode"] == "rank":
+                g5 = RenderGroup.rank(s5, world, rank, uids[2], scene=scene, receiver=receiver)
+            else:
+                g5 = RenderGroup(s5, devices=plan["devices"], scene=scene, receiver=receiver)
+        g5.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        moving = moving_listener(g5, ranks, args.c5_frames, int(np.prod(C5["rays"])) // world)
+        g5.close()
     bpb = bytes_per_bounce(n_tris)
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
     traffic, traffic_why = profile_guard(load_profile(os.path.join("r03", "trace_traffic.json")), args.workload, st0)
@@ -655,10 +686,12 @@ def main(argv=None) -> int:
         }
     if moving is not None:
         result["moving_listener"] = moving
-        if rank == 0 and world == 1 and not wl.get("total"):
-            shard = total_rays // 8
-            result["moving_listener_rank_of_8"] = moving_listener_rank_shape(settings, scene, receiver,
-                                                                             args.c5_frames, shard)
+        if rank == 0 and world == 1:
+            s5 = RenderSettings(rays=C5["rays"], ir_length_in_seconds=2, sample_rate=C5["sample_rate"], base_power=3.62,
+                                max_bounces=C5["max_bounces"], hrtf_absorption_rate=1.0, seed=1,
+                                device=plan["devices"][0])
+            result["moving_listener_rank_of_8"] = moving_listener_rank_shape(s5, scene, receiver, args.c5_frames,
+                                                                             int(np.prod(C5["rays"])) // 8)
     if pipelined is not None:
         result["pipelined"] = pipelined
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:

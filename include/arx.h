@@ -220,6 +220,18 @@ arx_renderer* arx_group_member(arx_group* g, int32_t i);
  * rank 0 builds and the tree goes to the other ranks with one RCCL broadcast over xGMI, so every
  * rank must call it (their arrays are not read). */
 arx_status arx_group_set_scene(arx_group* g, const float* tri_vertices, const float* tri_absorption, int64_t n_tris);
+/* The shard of rank `rank` of `n_ranks` in an n-ray launch: global ray ids [begin, end) =
+ * [rank*n/n_ranks, (rank+1)*n/n_ranks) (exact 128-bit products).  Host only; arx_group_render uses it. */
+void arx_group_shard(uint64_t n_rays, int32_t rank, int32_t n_ranks, uint64_t* begin, uint64_t* end);
+/* Tests only: arx_group_set_scene's one-GPU-per-process hand-over (rank 0 checks and builds the
+ * scene, the other ranks read its broadcast byte image; a failure on any rank fails the call on all)
+ * over a caller's transport instead of RCCL.  word(ctx, v, op): op 0 = broadcast *v from rank 0,
+ * op 1 = all-reduce max into *v; bytes(ctx, buf, n): broadcast n bytes from rank 0's buf into every
+ * rank's; both collective, 0 on success.  Host only; tree_hash = the tree every rank now holds. */
+typedef int (*arx_share_u64_fn)(void* ctx, uint64_t* value, int op);
+typedef int (*arx_share_bytes_fn)(void* ctx, uint8_t* buf, uint64_t n);
+arx_status arx_debug_share_scene(int32_t rank, const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
+                                 arx_share_u64_fn word, arx_share_bytes_fn bytes, void* ctx, uint64_t* tree_hash);
 /* The single-renderer setters, applied to every member. */
 arx_status arx_group_set_receiver_model(arx_group* g, int side, const float* tri_vertices_local, int64_t n_tris);
 arx_status arx_group_set_emitter(arx_group* g, float x, float y, float z);
@@ -319,14 +331,6 @@ arx_status arx_debug_set_leaf_max(int32_t leaf_max);
 arx_status arx_debug_wide_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
                                 const float* emitter, int64_t n_rays, int32_t bounces, uint64_t seed, double* out,
                                 size_t n_out);
-/* Host only: the scene's 16-bit BVH2 and its compact copy (B16: one 16-B unit per node, 8-bit planes
- * on frames shared by blocks of 2^block_bits units) traversed on the CPU in the trace kernel's order
- * over the same bouncing rays; out[11]: [0] queries, [1] / [2] BVH2 node steps / triangle tests per
- * query, [3] / [4] the same for B16, [5] B16 frame switches per query, [6] queries whose closest hits
- * differ, [7] B16 units, [8] B16 blocks, [9] BVH2 nodes, [10] 1 if the layout succeeded. */
-arx_status arx_debug_b16_stats(const float* tri_vertices, const float* tri_absorption, int64_t n_tris,
-                              const float* emitter, int64_t n_rays, int32_t bounces, uint64_t seed,
-                              int32_t block_bits, double* out, size_t n_out);
 /* Profiling builds only (ARX_TRACE_PROF=1, tools/trace_profile.py): the last trace launch's
  * per-wave records, 16 uint64 per wave (start / end shader clock, rays, queries, node-step slots
  * and lane-steps, leaf phases and lanes, shade phases and lanes, loop iterations, the time the

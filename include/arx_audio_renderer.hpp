@@ -1,20 +1,29 @@
 // arx_audio_renderer.hpp -- header-only C++ shim with the reference's AudioRenderer surface
 // (R/prebuild/obj_raytracer/AudioRenderer.h:16-152) over the libarx.so C ABI (arx.h).
 //
-// A main.cpp-style caller keeps its call sites:
-//     AudioRenderer* r = new AudioRenderer(scene_tris, ir_length_in_seconds, sample_rate, materials, rays);
+// A main.cpp-style caller keeps its call sites (main.cpp:40-67, 411-436, 547-587, 653-718):
+//     OptixModel* scene = new OptixModel{loadOBJ(path)};
+//     AudioRenderer* r = new AudioRenderer(scene, ir_length_in_seconds, sample_rate, materials, rays);
 //     r->setMonoOutput(mono); r->setBasePower(bp); r->setThresholds(thr, max_b);
-//     r->setEmitterPosInOptix(emitter); r->setSphereCenterInOptix(camera_pos);
-//     r->render(&ms); r->convoluteAudioFile(samples, bytes, outL, outR, &conv_ms, &proc_ms);
-// Differences (documented in INTEGRATION.md): the scene is passed as flat triangles with
-// material names instead of an OptixModel*, errors throw arx::Error (the reference
-// throws std::runtime_error / exit()s), setters take effect at the next render
-// without a full reload(), and a device list shards the rays over several GPUs (the
-// renderer always runs through libarx's group API: arx_group_*, RCCL).
+//     r->setEmitterPosInOptix(glm::vec3(...));
+//     placeReceiver(sphere, scene, camera_central_point, camera.globalAngle);
+//     r->setSphereCenterInOptix(glm::vec3(camera...)); r->render(&ms);
+//     r->full_render_cycle(&mutex, sphere, scene, camera_central_point, angle, samples, bytes, outL, outR);
+//     r->convoluteAudioFile(samples, bytes, outL, outR, &conv_ms, &proc_ms);
+// Vector arguments are any type with float members x, y, z (glm::vec3, gdt::vec3f, arx::Vec3).
+// placeReceiver records the receiver halves and pose in the OptixModel, as the reference's does, and
+// the renderer bound to that model picks them up at the next setSphereCenterInOptix -- with a device
+// refit of the receiver instead of a full GAS rebuild (OptixModel.cpp:153-257, AudioRenderer.cpp:466-486).
+// Differences (documented in INTEGRATION.md): errors throw arx::Error (the reference throws
+// std::runtime_error / exit()s), setters take effect at the next render without a full reload(), and
+// a device list shards the rays over several GPUs (the renderer always runs through libarx's group
+// API: arx_group_*, RCCL).
 #pragma once
 
 #include <chrono>
 #include <cstddef>
+#include <mutex>
+#include <type_traits>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -52,8 +61,59 @@ struct Mesh {
     std::string material_name;
 };
 
+// Any vector type with float members x, y, z (glm::vec3, gdt::vec3f, Vec3).
+template <class V3>
+using if_vec3 = std::enable_if_t<std::is_convertible<decltype(std::declval<const V3&>().x), float>::value &&
+                                 std::is_convertible<decltype(std::declval<const V3&>().z), float>::value>;
+template <class V3>
+inline Vec3 to_vec3(const V3& v) {
+    return Vec3{(float)v.x, (float)v.y, (float)v.z};
+}
+
+// HalfSphere (HalfSphere.h: one receiver half, loaded from leftHalf.obj / rightHalf.obj in its
+// local frame) and Sphere (Sphere.h:6-16: the two halves).
+using HalfSphere = Mesh;
+struct Sphere {
+    Sphere(const HalfSphere* left, const HalfSphere* right) : left_side(left), right_side(right) {}
+    const HalfSphere* left_side;
+    const HalfSphere* right_side;
+};
+
+// OptixModel (OptixModel.h:21-35): the scene's meshes, plus what placeReceiver last put in it -- the
+// receiver halves and the camera pose they were placed at.
+struct OptixModel {
+    std::vector<Mesh> meshes;
+    const HalfSphere* receiver[2] = {nullptr, nullptr};
+    Vec3 receiver_position{0.f, 0.f, 0.f};
+    float receiver_rotation = 0.f;  // degrees, Camera::globalAngle
+    uint64_t placements = 0;
+};
+
+// placeReceiver(Sphere, OptixModel*, vec3f cameraPosition, float rotation) (OptixModel.cpp:153-157):
+// the halves placed at the camera, rotated by -rotation about +Y.  Here it records them; the renderer
+// bound to the model re-places its receiver on the device at the next setSphereCenterInOptix.
+template <class V3, class = if_vec3<V3>>
+inline void placeReceiver(const Sphere& sphere, OptixModel* model, const V3& camera, float rotation) {
+    model->receiver[0] = sphere.left_side;
+    model->receiver[1] = sphere.right_side;
+    model->receiver_position = to_vec3(camera);
+    model->receiver_rotation = rotation;
+    ++model->placements;
+}
+
 class AudioRenderer {
   public:
+    // AudioRenderer(const OptixModel*, unsigned ir_length_in_seconds, int sample_rate,
+    //               std::vector<Material>, gdt::vec3f rays_per_dimension)   (AudioRenderer.h:24), on
+    // device 0 (AudioRenderer.cpp:252) or a list of GPUs; bound to the model's receiver placements
+    template <class V3, class = if_vec3<V3>>
+    AudioRenderer(const OptixModel* model, unsigned ir_length_in_seconds, int sample_rate,
+                  std::vector<Material> materials, V3 rays_per_dimension,
+                  const std::vector<int32_t>& devices = std::vector<int32_t>{0}, uint64_t seed = 1)
+        : AudioRenderer(model->meshes, ir_length_in_seconds, sample_rate, materials, to_vec3(rays_per_dimension),
+                        devices, seed) {
+        model_ = model;
+    }
     // AudioRenderer(const OptixModel*, unsigned ir_length_in_seconds, int sample_rate,
     //               std::vector<Material>, gdt::vec3f rays_per_dimension)   (AudioRenderer.h:24)
     // on one GPU (the reference hard-codes device 0, AudioRenderer.cpp:252) ...
@@ -151,8 +211,32 @@ class AudioRenderer {
     }
 
     void setEmitterPosInOptix(Vec3 p) { check(arx_group_set_emitter(g_, p.x, p.y, p.z)); }  // :33
+    template <class V3, class = if_vec3<V3>>
+    void setEmitterPosInOptix(const V3& p) {  // setEmitterPosInOptix(glm::vec3) (AudioRenderer.h:33)
+        setEmitterPosInOptix(to_vec3(p));
+    }
     // placeReceiver(sphere, model, camera, yaw) + setSphereCenterInOptix(camera) in one call
-    void setSphereCenterInOptix(Vec3 p, float yaw_deg = 0.0f) { check(arx_group_set_listener(g_, p.x, p.y, p.z, yaw_deg)); }
+    void setSphereCenterInOptix(Vec3 p, float yaw_deg) { check(arx_group_set_listener(g_, p.x, p.y, p.z, yaw_deg)); }
+    // setSphereCenterInOptix(glm::vec3) (AudioRenderer.h:35): the listener at p; on a renderer bound to
+    // an OptixModel, the receiver halves and rotation of the model's last placeReceiver (a new pair of
+    // halves is uploaded once), else the receiver model set by setReceiverModel at yaw 0
+    void setSphereCenterInOptix(Vec3 p) {
+        float yaw = 0.0f;
+        if (model_ && model_->placements) {
+            if (model_->receiver[0] && model_->receiver[1] &&
+                (model_->receiver[0] != bound_[0] || model_->receiver[1] != bound_[1])) {
+                setReceiverModel(*model_->receiver[0], *model_->receiver[1]);
+                bound_[0] = model_->receiver[0];
+                bound_[1] = model_->receiver[1];
+            }
+            yaw = model_->receiver_rotation;
+        }
+        setSphereCenterInOptix(p, yaw);
+    }
+    template <class V3, class = if_vec3<V3>>
+    void setSphereCenterInOptix(const V3& p) {
+        setSphereCenterInOptix(to_vec3(p));
+    }
     void setThresholds(float energy, unsigned int max_bounces) { check(arx_group_set_thresholds(g_, energy, max_bounces)); }
     void set_hrtf_absorption_rate(float v) { check(arx_group_set_hrtf_absorption_rate(g_, v)); }
     void setBasePower(float v) { check(arx_group_set_base_power(g_, v)); }
@@ -161,7 +245,25 @@ class AudioRenderer {
     // compatibility, it does nothing (the live path zips L/R in pass_d_live)
     void normalizeAndMergeStereoOutput(double*, double*, size_t, double*) {}
 
-    // full_render_cycle (AudioRenderer.cpp:790-798) minus the mutex (callers keep theirs)
+    // full_render_cycle(std::mutex*, Sphere, OptixModel*, gdt::vec3f, float, float*, size_t, float*,
+    // float*) (AudioRenderer.h:49, AudioRenderer.cpp:790-798): under the caller's mutex, place the
+    // receiver at the camera, move the listener there, render, convolve the file
+    template <class V3, class = if_vec3<V3>>
+    void full_render_cycle(std::mutex* mutex, const Sphere& sphere, OptixModel* scene, const V3& camera_central_point,
+                           float camera_global_angle, float* audio_samples, size_t size_of_audio,
+                           float* outputBuffer_left, float* outputBuffer_right) {
+        std::lock_guard<std::mutex> lock(*mutex);
+        if (scene && scene == model_) {
+            placeReceiver(sphere, scene, camera_central_point, camera_global_angle);
+            setSphereCenterInOptix(to_vec3(camera_central_point));
+        } else {  // a renderer not bound to this model: the halves and pose straight from the arguments
+            if (sphere.left_side && sphere.right_side) setReceiverModel(*sphere.left_side, *sphere.right_side);
+            setSphereCenterInOptix(to_vec3(camera_central_point), camera_global_angle);
+        }
+        render();
+        convoluteAudioFile(audio_samples, size_of_audio, outputBuffer_left, outputBuffer_right);
+    }
+    // the same without the mutex and the Sphere (callers that keep their own lock)
     void full_render_cycle(Vec3 camera, float yaw_deg, float* audio, size_t bytes, float* outL, float* outR) {
         setSphereCenterInOptix(camera, yaw_deg);
         render();
@@ -196,6 +298,8 @@ class AudioRenderer {
   private:
     arx_group* g_ = nullptr;
     arx_renderer* h_ = nullptr;  // member 0, owned by g_
+    const OptixModel* model_ = nullptr;        // the model whose receiver placements this renderer follows
+    const HalfSphere* bound_[2] = {nullptr, nullptr};  // the halves uploaded last
     size_t ir_length_ = 0;
     std::vector<double> live_scratch_;
     bool write_ir_ = false, write_output_ = false, experimentation_ = false;

@@ -136,39 +136,3 @@ def test_cw4_collapse_finds_the_same_closest_hits(which, c1_scene):
     assert st["mismatches"] == 0 and st["quantize_failures"] == 0
     assert st["q4_steps"] < st["q2_steps"]
     assert st["q4_depth"] < st["q2_depth"] + 2
-
-
-def b16_stats(tri_v, tri_abs, emitter, n_rays=400, bounces=8, seed=5, block_bits=6):
-    """arx_debug_b16_stats: the 16-bit BVH2 and its 16-B-per-node copy (B16: 8-bit planes on
-    block frames, arx_b16.cpp) traversed on the CPU in the kernel's order over the same rays."""
-    import ctypes as C
-
-    from audiorenderingv2_amd import _lib
-
-    tv = np.ascontiguousarray(tri_v, np.float32)
-    ta = np.ascontiguousarray(tri_abs, np.float32)
-    em = np.asarray(emitter, np.float32)
-    out = np.zeros(11)
-    _lib.check(_lib.lib().arx_debug_b16_stats(_lib.fptr(tv), _lib.fptr(ta), ta.size, _lib.fptr(em), n_rays, bounces,
-                                              seed, block_bits, out.ctypes.data_as(C.POINTER(C.c_double)), 11))
-    return dict(zip(["queries", "q2_steps", "q2_tris", "b16_steps", "b16_tris", "b16_frame_switches", "mismatches",
-                     "b16_units", "b16_blocks", "q2_nodes", "layout_ok"], out))
-
-
-@pytest.mark.parametrize("block_bits", [4, 6, 8])
-@pytest.mark.parametrize("which", ["c1", "soup"])
-def test_b16_copy_finds_the_same_closest_hits(which, block_bits, c1_scene):
-    """The B16 copy re-rounds the 16-bit planes outward onto 8-bit block frames: every query's
-    closest hit is the BVH2's, and the looser boxes can only add node steps and triangle tests."""
-    rng = np.random.default_rng(12)
-    if which == "c1":
-        tv, ta, em = c1_scene.tri_v, c1_scene.tri_abs, (0.5, 3.0, 1.0)
-    else:
-        tv = rng.uniform(-5, 5, (3000, 9)).astype(np.float32)
-        tv[::17, 3:6] = tv[::17, 0:3]
-        ta, em = np.full(len(tv), 0.2, np.float32), (0.1, 0.2, 0.3)
-    st = b16_stats(tv, ta, em, block_bits=block_bits)
-    assert st["layout_ok"] == 1.0 and st["queries"] > 400
-    assert st["mismatches"] == 0
-    assert st["b16_steps"] >= st["q2_steps"] and st["b16_tris"] >= st["q2_tris"]
-    assert st["b16_units"] % (1 << block_bits) == 0 and st["b16_blocks"] == st["b16_units"] / (1 << block_bits)

@@ -133,3 +133,46 @@ def test_scene_image_roundtrip_and_hash(c1_scene):
     bad[0] = 1.5  # absorption outside [0, 1]
     h, n = C.c_uint64(), C.c_uint64()
     assert L.arx_debug_scene_roundtrip(_lib.fptr(tv), _lib.fptr(bad), bad.size, C.byref(h), C.byref(n)) == 1
+
+
+@pytest.mark.parametrize("case", ["ok", "root_fails", "stage_fails", "consume_fails", "rank0_skips"])
+def test_rank_path_scene_share_protocol(case, tmp_path):
+    """arx_group_set_scene's rank path (arx_scene_share.hpp) with three ranks as threads: a failed
+    input check or build on rank 0, a rank that cannot stage the image and a rank that cannot read it
+    make every rank return the same error instead of leaving the others in a collective.  The
+    round-3 shape -- rank 0 returning before the first collective -- hangs (the watchdog's exit 2)."""
+    import shutil
+    import subprocess
+
+    gxx = shutil.which("g++")
+    if not gxx:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "scene_share_test")
+    subprocess.run([gxx, "-O1", "-std=c++17", "-pthread", "-Wall", "-Werror", "-I",
+                    os.path.join(REPO, "audiorenderingv2_amd", "csrc"),
+                    os.path.join(REPO, "tests", "cpp", "scene_share_test.cpp"), "-o", exe], check=True)
+    res = subprocess.run([exe, case], capture_output=True, text=True, timeout=60)
+    if case == "rank0_skips":
+        assert res.returncode == 2 and "HANG" in res.stdout, res.stdout
+    else:
+        want = {"ok": "ok", "root_fails": "root_failed", "stage_fails": "staging_failed",
+                "consume_fails": "consume_failed"}[case]
+        assert res.returncode == 0, res.stdout
+        assert res.stdout.count(f": {want} ") == 3, res.stdout
+
+
+def test_main_style_caller_compiles_against_reference_glm(tmp_path):
+    """main.cpp:40-67's full_render over the C++ shim builds with the reference's own glm::vec3 (the
+    glm the reference vendors, read in place; this container only) and links against libarx.so.
+    The GPU run of the same program is tests/test_gpu_shim.py::test_main_style_full_render_matches_oracle."""
+    import shutil
+    import subprocess
+
+    glm = "/root/reference/prebuild/common"
+    gxx = shutil.which("g++")
+    if not gxx or not os.path.exists(os.path.join(glm, "glm", "glm.hpp")):
+        pytest.skip("g++ or the reference's glm not available")
+    pkg = os.path.join(REPO, "audiorenderingv2_amd")
+    subprocess.run([gxx, "-std=c++17", "-O1", "-Wall", "-Werror", "-DARX_DEMO_GLM", "-I", glm, "-I",
+                    os.path.join(REPO, "include"), os.path.join(REPO, "tests", "cpp", "main_style_demo.cpp"),
+                    "-L", pkg, "-larx", f"-Wl,-rpath,{pkg}", "-o", str(tmp_path / "main_style_demo")], check=True)

@@ -208,3 +208,59 @@ def test_cpp_shim_c4_sharded_equals_python_group(demo):
     assert 20 * 10_000_000 < gst["queries"] <= 32 * 10_000_000 and gst["receiver_hits"] > 10000
     assert np.array_equal(np.fromfile(out / "ir_left.f32", np.float32).view(np.uint32), gl.view(np.uint32))
     assert np.array_equal(np.fromfile(out / "ir_right.f32", np.float32).view(np.uint32), gr.view(np.uint32))
+
+
+def test_main_style_full_render_matches_oracle(demo):
+    """main.cpp:40-67's full_render, unchanged, over the shim (tests/cpp/main_style_demo.cpp): an
+    OptixModel*, a Sphere of two HalfSpheres, a gdt::vec3f camera point and glm::vec3 setters.  The file
+    branch (full_render_cycle under the caller's mutex) renders with the receiver placed at the camera
+    and rotated by its angle, then convolves; the live branch (placeReceiver + setSphereCenterInOptix +
+    render) follows a moved, turned camera.  Both IRs bit-exact vs the oracle at those poses, the
+    convolution <= 1 ULP(max)."""
+    d, _ = demo
+    exe = str(d / "main_style_demo")
+    pkg = os.path.join(REPO, "audiorenderingv2_amd")
+    subprocess.run([shutil.which("g++"), "-std=c++17", "-O2", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "cpp", "main_style_demo.cpp"), "-L", pkg, "-larx",
+                    f"-Wl,-rpath,{pkg}", "-o", exe], check=True)
+    meshes = load_meshes_npz(os.path.join(GOLDEN, "test_obj.npz"))
+    write_obj(str(d / "room2.obj"), meshes, "room2.mtl")
+    write_receivers(d)
+    sr = 16000
+    x = (0.3 * np.sin(2 * np.pi * 220 * np.arange(2 * sr + 99) / sr)).astype(np.float32)
+    save_wav(str(d / "in2.wav"), x, sr, 32)
+    mats = reference_config_materials()
+    emitter, listener, angle = (0.5, 3.0, 1.0), (2.5, 9.9, 0.0), 40.0
+    cfg = {
+        "renderer_parameters": {"ir_length_in_seconds": 2},
+        "scene_parameters": {"mono": False, "scene_file_path": str(d / "room2.obj"), "audio_file_path": str(d / "in2.wav"),
+                             "initial_receiver_pos": dict(zip("xyz", listener)),
+                             "initial_emitter_pos": dict(zip("xyz", emitter))},
+        "pathtracer_parameters": {"base_power": 3.62, "rays": {"x": 64, "y": 64, "z": 8}, "ray_energy_threshold": 0.0,
+                                  "ray_max_bounces": 8, "hrtf_absorption_rate": 0.25,
+                                  "materials": [{"name": n, "mat_absorption": a} for n, a in mats]},
+    }
+    (d / "config2.json").write_text(json.dumps(cfg))
+    out = d / "out_main"
+    out.mkdir()
+    run = subprocess.run([exe, str(d / "config2.json"), str(d / "leftHalf.obj"), str(d / "rightHalf.obj"), str(out),
+                          str(angle)], capture_output=True, text=True, timeout=120)
+    assert run.returncode == 0, run.stderr
+    scene = scene_from_meshes(meshes, mats)
+    moved = (np.float32(listener[0]) + np.float32(0.5), listener[1], np.float32(listener[2]) - np.float32(0.25))
+    for tag, pos, yaw in (("file", listener, angle), ("live", moved, angle + 30.0)):
+        tv, ta = world_scene(scene, tuple(float(c) for c in pos), yaw)
+        p = po.make_params(rays=(64, 64, 8), sample_rate=sr, base_power=float(np.float32(3.62)), max_bounces=8,
+                           hrtf=0.0, emitter=emitter, listener=tuple(float(c) for c in pos))
+        hl, hr, ost = po.Scene(tv, ta, bvh=True).trace(p, threads=8)
+        ol, orr = po.finalize_ir(p, hl, hr)
+        assert ost["receiver_hits"] > 0, tag
+        gl = np.fromfile(out / f"ir_{tag}_left.f32", np.float32)
+        gr = np.fromfile(out / f"ir_{tag}_right.f32", np.float32)
+        assert np.array_equal(gl.view(np.uint32), ol.view(np.uint32)), tag
+        assert np.array_equal(gr.view(np.uint32), orr.view(np.uint32)), tag
+        if tag == "file":
+            for ch, ir in (("left", ol), ("right", orr)):
+                got = np.fromfile(out / f"conv_{ch}.f32", np.float32)
+                ref = po.convolute_audio(x, sr, ir)
+                assert np.abs(got - ref).max() <= np.spacing(np.float32(np.abs(ref).max()))
