@@ -68,6 +68,7 @@ def bytes_per_bounce(n_tris: int) -> int:
 
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
 NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2", 2: "4-wide compressed (CW4)"}  # arx_stats.trace_format
+PROFILES = "r04"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
 
 
 # ----------------------------------------------------------------------------- rank plumbing ---
@@ -567,11 +568,11 @@ def main(argv=None) -> int:
         g5.close()
     bpb = bytes_per_bounce(n_tris)
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
-    traffic, traffic_why = profile_guard(load_profile(os.path.join("r03", "trace_traffic.json")), args.workload, st0)
-    counts, counts_why = profile_guard(load_profile(os.path.join("r03", "trace_counts_c3.json")), args.workload, st0,
+    traffic, traffic_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_traffic.json")), args.workload, st0)
+    counts, counts_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_counts_c3.json")), args.workload, st0,
                                        ("workload", "tree_hash", "trace_kernel_id"))
-    td, td_why = profile_guard(load_profile(os.path.join("r03", "trace_td_c3.json")), args.workload, st0)
-    vmem, vmem_why = profile_guard(load_profile(os.path.join("r03", "trace_vmem_ceiling.json")), args.workload, st0)
+    td, td_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_td_c3.json")), args.workload, st0)
+    vmem, vmem_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_vmem_ceiling.json")), args.workload, st0)
     conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02m.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
@@ -615,12 +616,17 @@ def main(argv=None) -> int:
         "roofline": {
             "kernel": "trace_kernel",
             "bound": "hbm",
+            "convention": "SURVEY.md §8d algorithmic bytes per ray-bounce (32 + 32 + 64 ceil(log2 T) + 48); the "
+                          "tree is cache-resident, so this is a byte convention, not the binding unit: the "
+                          "kernel is co-limited by the vector-memory return path and VALU issue (roofline_td, "
+                          "roofline_valu)",
+            "binding_units": "td+valu",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
-            "traffic_source": "profiles/r03/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
+            "traffic_source": f"profiles/{PROFILES}/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
                               "build, tree and workload; PMC counters cannot be read inside this run): " + traffic_why,
             "algorithmic_bytes_per_bounce": bpb,
             "trace_launch_ms": trace_ms,
@@ -652,7 +658,7 @@ def main(argv=None) -> int:
             "note": "peak = independent one-block-per-lane gathers at this hit mix (tools/td_microbench.hip); "
                     "shared nodes and same-block node halves let the kernel pass it",
             "mix": {"l1": vmem["fraction_l1"], "l2_hit": vmem["fraction_l2_hit"], "l2_miss": vmem["fraction_l2_miss"]},
-            "source": "profiles/r03/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix): " + vmem_why,
+            "source": f"profiles/{PROFILES}/trace_vmem_ceiling.json (tools/td_microbench.hip rates + PMC mix): " + vmem_why,
         }
     else:
         result["roofline_vmem"] = None
@@ -682,7 +688,7 @@ def main(argv=None) -> int:
             "lane_loads_16B_per_query": counts["lane_loads_16B_per_query"],
             "lane_loads_per_s": lanes / (trace_ms * 1e-3),
             "l1_side_GBps": 16 * lanes / (trace_ms * 1e-3) / 1e9,
-            "source": "profiles/r03/trace_counts_c3.json (counting build, tools/trace_counts.py): " + counts_why,
+            "source": f"profiles/{PROFILES}/trace_counts_c3.json (counting build, tools/trace_counts.py): " + counts_why,
         }
     if moving is not None:
         result["moving_listener"] = moving

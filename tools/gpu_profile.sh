@@ -1,13 +1,13 @@
-# Round-3 measurement pass on one MI355X: bench line, rocprofv3 kernel stats of the same command,
+# Measurement pass on one MI355X: bench line, rocprofv3 kernel stats of the same command,
 # PMC traffic (FETCH_SIZE / WRITE_SIZE, separate passes), pipeline state counters, the counting
 # build's lane loads per query, and the guarded profile JSONs bench.py reads (tree hash + VGPRs).
-# Outputs under gpurun_out/r03/.  TAG names the files.
+# Outputs under gpurun_out/$RD/ (default r04).  TAG names the files.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=gpurun_out/r03
-TAG=${TAG:-r03}
+O=gpurun_out/${RD:-r04}
+TAG=${TAG:-r04}
 mkdir -p $O
 timeout -k 10 400 python3 bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo "bench failed"; tail -20 $O/bench_$TAG.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --c5-frames 0 --no-pipelined --no-streaming > $O/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof_$TAG.log; exit 1; }

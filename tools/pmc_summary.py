@@ -49,7 +49,8 @@ def main():
                # fraction over the kernel's cycles (GRBM_GUI_ACTIVE / 8 = cycles per XCD)
                "kernel_cycles_per_xcd": g,
                "valu_busy_per_simd_cycle": c["SQ_INSTS_VALU"] * 4.0 / (cus * 4) / g,
-               "source": sys.argv[2]}
+               # the tracked copy bench.py reads (the tool writes under gpurun_out/ on the GPU box)
+               "source": "profiles/" + sys.argv[2].split("gpurun_out/", 1)[-1]}
         with open(sys.argv[2], "w") as fh:
             json.dump(out, fh, indent=1)
     for variant, c in sorted(data.items()):
