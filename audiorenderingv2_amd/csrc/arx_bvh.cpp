@@ -10,7 +10,6 @@
 #include "arx_bvh.hpp"
 
 #include <algorithm>
-#include <queue>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -681,10 +680,6 @@ int64_t rotation_pass(BvhBuild& b, int cap) {
 }
 }  // namespace
 
-namespace {
-void renumber_preorder(BvhBuild& b);
-}  // namespace
-
 void rotate_tree(BvhBuild& b, int passes) {
     if (passes <= 0 || !is_inner(b.root)) return;
     std::vector<int> h;
@@ -696,14 +691,9 @@ void rotate_tree(BvhBuild& b, int passes) {
         if (n == 0) break;
     }
     if (total == 0) return;
-    renumber_preorder(b);
-}
-
-namespace {
-// After rotations or re-insertions moved subtrees under other parents: renumber the nodes in
-// depth-first pre-order (child 0 first, as the builder allocates them), so every parent precedes its
-// children again (validate_bvh, bfs_prefix_order and the receiver refit's level schedule rely on it).
-void renumber_preorder(BvhBuild& b) {
+    // Rotations move subtrees under other parents: renumber the nodes in depth-first pre-order
+    // (child 0 first, as the builder allocates them), so every parent precedes its children again
+    // (validate_bvh, bfs_prefix_order and the receiver refit's level schedule rely on it).
     std::vector<int32_t> order, st{b.root.ref};
     order.reserve(b.nodes.size());
     while (!st.empty()) {
@@ -726,202 +716,6 @@ void renumber_preorder(BvhBuild& b) {
     }
     b.nodes.swap(out);
     b.root.ref = remap[(size_t)b.root.ref];
-}
-
-// ---- insertion-based optimisation (Bittner, Hapala & Havran 2013) ----
-// The tree as slots: node v's child s, or the root slot (node -1).  parent[v] is the slot inner node
-// v hangs in; h[v] the levels of inner nodes in v's subtree (1: only leaves below), so the subtree at
-// depth d (the root node at 1) reaches depth d + h[v] - 1, which must stay <= cap.
-struct Slot {
-    int32_t node;
-    int s;
-};
-
-struct Reinserter {
-    BvhBuild& b;
-    int cap;
-    float inv_seg;  // 2 / segment length (0: pure half-area)
-    std::vector<Slot> parent;
-    std::vector<int> h;
-
-    float cost(const ChildRef& c) const {
-        const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
-        return dx * dy + dy * dz + dz * dx + inv_seg * dx * dy * dz;
-    }
-    explicit Reinserter(BvhBuild& bb, int c, float seg) : b(bb), cap(c), inv_seg(seg > 0.0f ? 2.0f / seg : 0.0f) {
-        parent.assign(b.nodes.size(), Slot{-1, 0});
-        for (size_t v = 0; v < b.nodes.size(); ++v)
-            for (int s = 0; s < 2; ++s) {
-                const ChildRef c2 = node_child(b.nodes[v], s);
-                if (is_inner(c2)) parent[(size_t)c2.ref] = Slot{(int32_t)v, s};
-            }
-        subtree_heights(b, h);
-    }
-    ChildRef get(Slot s) const { return s.node < 0 ? b.root : node_child(b.nodes[(size_t)s.node], s.s); }
-    void put(Slot s, const ChildRef& c) {
-        if (s.node < 0) b.root = c;
-        else set_node_child(b.nodes[(size_t)s.node], s.s, c);
-        if (is_inner(c)) parent[(size_t)c.ref] = s;
-    }
-    int hof(const ChildRef& c) const { return is_inner(c) ? h[(size_t)c.ref] : 0; }
-    // boxes (unions of the children's stored boxes) and heights from inner node v up to the root
-    void refit_up(int32_t v) {
-        while (v >= 0) {
-            const ChildRef c0 = node_child(b.nodes[(size_t)v], 0), c1 = node_child(b.nodes[(size_t)v], 1);
-            h[(size_t)v] = 1 + std::max(hof(c0), hof(c1));
-            const Slot ps = parent[(size_t)v];
-            const ChildRef me = unite(c0, c1, v);
-            if (ps.node < 0) b.root = me;
-            else set_node_child(b.nodes[(size_t)ps.node], ps.s, me);
-            v = ps.node;
-        }
-    }
-    // Take inner node n and its parent out (the sibling moves up into the parent's slot); n's two
-    // children are left to re-insert, n and its parent are free.  Only below the root's children.
-    bool remove(int32_t n, ChildRef* kids, int32_t* freed) {
-        const Slot sn = parent[(size_t)n];
-        const int32_t p = sn.node;
-        if (p < 0 || parent[(size_t)p].node < 0) return false;
-        const Slot sp = parent[(size_t)p];
-        put(sp, node_child(b.nodes[(size_t)p], 1 - sn.s));
-        refit_up(sp.node);
-        kids[0] = node_child(b.nodes[(size_t)n], 0);
-        kids[1] = node_child(b.nodes[(size_t)n], 1);
-        freed[0] = n;
-        freed[1] = p;
-        return true;
-    }
-    // Re-insert subtree a with the free node f as its new parent, at the slot where the union with
-    // what hangs there adds the least inner-node area (the new node's area plus every ancestor's
-    // growth), within the depth cap.  False if no slot keeps the cap.
-    bool insert(const ChildRef& a, int32_t f) {
-        struct E {
-            float lb, induced;
-            Slot s;
-            int d;
-            bool operator<(const E& o) const { return lb > o.lb; }  // min-heap on the bound
-        };
-        const float aa = cost(a);
-        const int ha = hof(a);
-        std::priority_queue<E> pq;
-        pq.push(E{aa, 0.0f, Slot{-1, 0}, 1});
-        float best = std::numeric_limits<float>::infinity();
-        Slot best_s{-2, 0};
-        while (!pq.empty()) {
-            const E e = pq.top();
-            pq.pop();
-            if (e.lb >= best) break;
-            const ChildRef x = get(e.s);
-            const float direct = cost(unite(x, a, -1));
-            const float total = e.induced + direct;
-            if (e.d + std::max(hof(x), ha) <= cap && total < best) {
-                best = total;
-                best_s = e.s;
-            }
-            if (is_inner(x) && e.d + 1 + ha <= cap) {
-                const float ind = e.induced + direct - cost(x);
-                if (ind + aa < best)
-                    for (int s = 0; s < 2; ++s) pq.push(E{ind + aa, ind, Slot{x.ref, s}, e.d + 1});
-            }
-        }
-        if (best_s.node < -1) return false;
-        const ChildRef x = get(best_s);
-        BvhNode& nf = b.nodes[(size_t)f];
-        set_node_child(nf, 0, x);
-        set_node_child(nf, 1, a);
-        if (is_inner(x)) parent[(size_t)x.ref] = Slot{f, 0};
-        if (is_inner(a)) parent[(size_t)a.ref] = Slot{f, 1};
-        h[(size_t)f] = 1 + std::max(hof(x), ha);
-        put(best_s, unite(x, a, f));
-        refit_up(best_s.node);
-        return true;
-    }
-};
-}  // namespace
-
-double inner_area_sum(const BvhBuild& b) {
-    double s = is_inner(b.root) ? half_area(b.root) : 0.0;
-    for (const BvhNode& n : b.nodes)
-        for (int k = 0; k < 2; ++k) {
-            const ChildRef c = node_child(n, k);
-            if (is_inner(c)) s += half_area(c);
-        }
-    return s;
-}
-
-double inner_cost_sum(const BvhBuild& b, float seg) {
-    const float inv_seg = seg > 0.0f ? 2.0f / seg : 0.0f;
-    auto cost = [&](const ChildRef& c) {
-        const double dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
-        return dx * dy + dy * dz + dz * dx + inv_seg * dx * dy * dz;
-    };
-    double s = is_inner(b.root) ? cost(b.root) : 0.0;
-    for (const BvhNode& n : b.nodes)
-        for (int k = 0; k < 2; ++k) {
-            const ChildRef c = node_child(n, k);
-            if (is_inner(c)) s += cost(c);
-        }
-    return s;
-}
-
-void reinsert_tree(BvhBuild& b, int batches, float fraction, double* area_before, double* area_after) {
-    const float seg = build_params().reinsert_seg;
-    const double a0 = inner_cost_sum(b, seg);
-    if (area_before) *area_before = a0;
-    if (area_after) *area_after = a0;
-    if (batches <= 0 || !is_inner(b.root) || b.nodes.size() < 8) return;
-    for (const BvhNode& n : b.nodes)  // empty children only in degenerate trees: leave those alone
-        if (n.d[2] < 0 || n.d[3] < 0) return;
-    std::vector<int> h0;
-    const int cap = subtree_heights(b, h0);
-    BvhBuild best = b;
-    double best_a = a0;
-    int stale = 0;
-    const size_t per_batch = std::max<size_t>(1, (size_t)(fraction * (double)b.nodes.size()));
-    for (int it = 0; it < batches && stale < 3; ++it) {
-        Reinserter R(b, cap, seg);
-        // the nodes worst by Bittner's combined measure: area x area / mean child area x area / min child area
-        std::vector<std::pair<float, int32_t>> m;
-        m.reserve(b.nodes.size());
-        for (size_t v = 0; v < b.nodes.size(); ++v) {
-            if (R.parent[v].node < 0 || R.parent[(size_t)R.parent[v].node].node < 0) continue;
-            const float av = R.cost(R.get(R.parent[v]));
-            const float c0 = R.cost(node_child(b.nodes[v], 0)), c1 = R.cost(node_child(b.nodes[v], 1));
-            const float msum = av / std::max(0.5f * (c0 + c1), 1e-30f), mmin = av / std::max(std::min(c0, c1), 1e-30f);
-            m.push_back({msum * mmin * av, (int32_t)v});
-        }
-        const size_t k = std::min(per_batch, m.size());
-        std::partial_sort(m.begin(), m.begin() + (std::ptrdiff_t)k, m.end(),
-                          [](const auto& x, const auto& y) { return x.first > y.first; });
-        std::vector<char> used(b.nodes.size(), 0);
-        bool ok = true;
-        for (size_t i = 0; i < k && ok; ++i) {
-            const int32_t n = m[i].second;
-            if (used[(size_t)n]) continue;  // reused as a new node earlier in this batch
-            ChildRef kids[2];
-            int32_t freed[2];
-            if (!R.remove(n, kids, freed)) continue;
-            used[(size_t)freed[0]] = used[(size_t)freed[1]] = 1;
-            // the larger subtree first (Bittner et al.)
-            if (R.cost(kids[1]) > R.cost(kids[0])) std::swap(kids[0], kids[1]);
-            ok = R.insert(kids[0], freed[0]) && R.insert(kids[1], freed[1]);
-        }
-        if (!ok) {  // no slot within the depth cap: back to the best tree so far
-            b = best;
-            break;
-        }
-        const double a = inner_cost_sum(b, seg);
-        if (a < best_a * (1.0 - 1e-4)) {
-            best_a = a;
-            best = b;
-            stale = 0;
-        } else {
-            ++stale;
-        }
-    }
-    b = best;
-    renumber_preorder(b);
-    if (area_after) *area_after = best_a;
 }
 
 void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, int64_t n, int32_t id_base,
@@ -960,7 +754,6 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
         out.tris.reserve((size_t)n + (size_t)sb.refs_left);
         out.root = sb.build(refs, 1);
         rotate_tree(out, sb.prm.rotation_passes);
-        reinsert_tree(out, sb.prm.reinsert_batches, sb.prm.reinsert_fraction);
         return;
     }
     Builder b;

@@ -35,9 +35,6 @@ struct BvhBuild {
 #ifndef ARX_BVH_ROTATIONS
 #define ARX_BVH_ROTATIONS 8
 #endif
-#ifndef ARX_BVH_REINSERT_BATCHES
-#define ARX_BVH_REINSERT_BATCHES 0
-#endif
 #ifndef ARX_SAH_LEAF_MAX
 #define ARX_SAH_LEAF_MAX 2
 #endif
@@ -77,16 +74,6 @@ struct BuildParams {
     // node between them, never deepening the tree past its built depth.  On the C3 scene: inner-
     // node SAH -2.7 %, node visits per query -3.7 % (tools/bvh_stats.cpp).
     int rotation_passes = ARX_BVH_ROTATIONS;
-    // Insertion-based optimisation after the rotations (Bittner, Hapala & Havran 2013): batches of
-    // the inner nodes worst by area ratio are taken out and their two subtrees re-inserted where they
-    // add the least inner-node area (branch and bound from the root), never past the built depth.
-    // reinsert_batches batches of reinsert_fraction of the inner nodes each; the best tree is kept.
-    int reinsert_batches = ARX_BVH_REINSERT_BATCHES;
-    float reinsert_fraction = 0.01f;
-    // The re-insertion's node cost: half-area + volume / reinsert_seg (<= 0: half-area alone, the
-    // SAH).  For segments of length l from origins inside the scene, a convex box is crossed with
-    // probability ~ (l/4) * area + volume (Crofton), i.e. half-area + 2 volume / l.
-    float reinsert_seg = 0.0f;
 };
 // Process-wide parameters: production defaults, never read from the environment; design tools
 // (tools/bvh_stats.cpp, tools/bvh_check.cpp) edit the struct before building.
@@ -100,12 +87,6 @@ void build_bvh(const float* tri_v, const float* tri_abs, float absorption_fill, 
 void relocate_bvh(BvhBuild& b, int32_t node_offset, int32_t tri_offset);
 // Tree rotations on a finished build (BuildParams::rotation_passes; the spatial builder runs them).
 void rotate_tree(BvhBuild& b, int passes);
-// Insertion-based optimisation of a finished build (BuildParams::reinsert_*; the spatial builder runs
-// it after the rotations).  Returns the inner-node area sum (the SAH traversal term) before and after.
-void reinsert_tree(BvhBuild& b, int batches, float fraction, double* area_before = nullptr,
-                   double* area_after = nullptr);
-// Sum of the inner nodes' box half-areas (the SAH traversal term, unnormalised).
-double inner_area_sum(const BvhBuild& b);
 // Renumber the nodes so the first k inner nodes in breadth-first order from the root take
 // indices 0..k-1 (the rest keep their order, so parents still precede their children): the
 // top levels of the scene tree share cache lines.

@@ -8,6 +8,7 @@
 //   g++ -O2 -std=c++17 -I audiorenderingv2_amd/csrc tools/bvh_stats.cpp \
 //       audiorenderingv2_amd/csrc/arx_bvh.cpp -o /tmp/bvh_stats
 //   /tmp/bvh_stats scene.f32 n_tris ex ey ez n_rays bounces
+// (The insertion-based optimisation tried in round 4 -- REINSERT / RESEG -- is at commit 198ae4a.)
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -165,18 +166,13 @@ int main(int argc, char** argv) {
     if (const char* e = std::getenv("SDEPTH")) bp.spatial_max_depth = std::atoi(e);
     if (const char* e = std::getenv("BUDGET")) bp.spatial_budget = (float)std::atof(e);
     if (const char* e = std::getenv("ROT")) bp.rotation_passes = std::atoi(e);
-    if (const char* e = std::getenv("REINSERT")) bp.reinsert_batches = std::atoi(e);
-    if (const char* e = std::getenv("REFRAC")) bp.reinsert_fraction = (float)std::atof(e);
-    if (const char* e = std::getenv("RESEG")) bp.reinsert_seg = (float)std::atof(e);
     std::printf("params: bins %d leaf_max %d trav %.2f isect %.2f rotation passes %d\n", bp.bins, bp.leaf_max, bp.trav_cost,
                 bp.isect_cost, bp.rotation_passes);
     BvhBuild b;
     std::vector<float> ab(n, 0.5f);
     const auto t_build = std::chrono::steady_clock::now();
     build_bvh(tv.data(), ab.data(), 0.5f, n, 0, b);
-    std::printf("build %.2f s, reinsert batches %d x %.3f, inner-node area sum %.6g\n",
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_build).count(), bp.reinsert_batches,
-                bp.reinsert_fraction, inner_area_sum(b));
+    std::printf("build %.2f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t_build).count());
     relocate_bvh(b, 1, 0);
     BvhNode top = make_node(b.root, empty_child());
     Tree t2 = from_binary(b.nodes, top);
