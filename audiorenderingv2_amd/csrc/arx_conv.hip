@@ -28,6 +28,7 @@
 // before the single f32 rounding (the "1 ULP of max|y|" bar of SURVEY.md §8c).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -865,6 +866,41 @@ struct MrArgs {
     int32_t chain;    // pass_c_chain: pairs per block
 };
 
+// Measurement builds only (build.py --exp cprof -D ARX_CONV_PROF=1, tools/conv_phases.py): per
+// workgroup of passes A / B / C, the 100-MHz device real-time counter at entry, after its loads
+// reached LDS, after its FFT and at its last store; kProfSlot words per workgroup, pass k's records
+// from k * kProfPass.  The product build compiles none of it.
+#ifndef ARX_CONV_PROF
+#define ARX_CONV_PROF 0
+#endif
+#if ARX_CONV_PROF
+constexpr int kProfSlot = 8, kProfPass = 4096 * kProfSlot;
+__device__ unsigned long long g_conv_prof[3 * kProfPass];
+struct ConvProf {
+    unsigned long long t[4] = {0, 0, 0, 0};
+    __device__ void mark(int k) { t[k] = __builtin_amdgcn_s_memrealtime(); }
+    // one word per lane of wave 0 (a vector store with per-lane addresses)
+    __device__ void flush(int pass) {
+        const int l = (int)threadIdx.x;
+        if (l >= kProfSlot) return;
+        const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v = l == k ? t[k] : v;
+        v = l == 4 ? (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) : v;  // XCC id
+        v = l == 5 ? (unsigned long long)wg : v;
+        if (wg < 4096) g_conv_prof[pass * kProfPass + wg * kProfSlot + l] = v;
+    }
+};
+#define CONV_PROF_DECL ConvProf prof_;
+#define CONV_PROF_MARK(k) prof_.mark(k)
+#define CONV_PROF_FLUSH(pass) prof_.flush(pass)
+#else
+#define CONV_PROF_DECL
+#define CONV_PROF_MARK(k)
+#define CONV_PROF_FLUSH(pass)
+#endif
+
 
 // dst[i] = src[i * stride], i < count <= 64 IT, by the nt >= 64 threads (all loads issued before
 // the LDS stores)
@@ -911,6 +947,8 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc, sc = mr_col_stride(N1, tc);
     double2* twl = lds + (size_t)tc * sc;
     double2* tr = twl + N1;
+    CONV_PROF_DECL
+    CONV_PROF_MARK(0);
     double2 v[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {  // every load in flight before the first use
@@ -945,8 +983,10 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
         if (n1 < N1) lds[(size_t)c * sc + n1] = v[it];
     }
     __syncthreads();
+    CONV_PROF_MARK(1);
     fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
+    CONV_PROF_MARK(2);
     double2* dst = MODE == 0 && ir ? a.G : ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
     // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r; this thread's column n2 is fixed and k1 steps
     // by 64, so (q, r) advance by (64 n2) div / mod N2 -- one division per thread, not per element
@@ -965,6 +1005,8 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
             ++q;
         }
     }
+    CONV_PROF_MARK(3);
+    if (MODE == 0) CONV_PROF_FLUSH(0);
 }
 
 // Pass B: per row k1 (one wave; nt / 64 rows per block): forward row FFT (N2); mode 1 stores it (IR
@@ -1082,6 +1124,8 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     const int u = (slot / batches) * 8 + xcd;  // mirror-row unit, dealt as pass_b_mr's row groups
     const int64_t batch = slot % batches;
     if (u >= units) return;  // the whole block: no barrier is reached
+    CONV_PROF_DECL
+    CONV_PROF_MARK(0);
     const bool self = u == 0;  // rows 0 and N1 / 2: each its own mirror
     const int k1 = w == 0 ? u : (self ? N1 / 2 : N1 - u);
     const bool live = !(self && w == 1 && (N1 & 1));  // odd N1: row 0 has no partner row
@@ -1118,6 +1162,7 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
         }
     }
     __syncthreads();
+    CONV_PROF_MARK(1);
     fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
     __syncthreads();  // the mirror row's G spectrum is complete
     double2 h0[IT], h1[IT];
@@ -1155,6 +1200,14 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     }
     __builtin_amdgcn_wave_barrier();
     fft2_wave_any<R7, LM, L2>(gbuf, spec, tw2, m.f2, j, +1);
+    CONV_PROF_MARK(2);
+#if ARX_CONV_PROF
+    if (!live) {
+        CONV_PROF_MARK(3);
+        CONV_PROF_FLUSH(1);
+        return;
+    }
+#endif
     if (!live) return;
     double2* dst0 = a.S + ((size_t)batch * 3 + 1) * a.M + (int64_t)k1 * N2;
     double2* dst1 = dst0 + a.M;
@@ -1168,6 +1221,8 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
             dst1[i] = cmul(spec[i], t);
         }
     }
+    CONV_PROF_MARK(3);
+    CONV_PROF_FLUSH(1);
 }
 
 // Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
@@ -1237,6 +1292,8 @@ __global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
     double2* twl = lds + (size_t)tc * sc;
     const int64_t sr = a.sr;
     float* out = ch == 0 ? a.out_l : a.out_r;
+    CONV_PROF_DECL
+    CONV_PROF_MARK(0);
     stage_table<IT>(twl, a.tw, N1, N2, nt);
     double2 v[IT];
     double fprev[IT];  // hi.y of the previous pair at this thread's (column, row) slots
@@ -1261,9 +1318,15 @@ __global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
             if (k1 < N1) lds[(size_t)c * sc + k1] = v[it];
         }
         __syncthreads();
+#if ARX_CONV_PROF
+        if (pair == pstart) CONV_PROF_MARK(1);
+#endif
         if (pair + 1 < p1) load(pair + 1);  // in flight during this pair's FFT
         fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, +1);
         __syncthreads();
+#if ARX_CONV_PROF
+        if (pair == pstart) CONV_PROF_MARK(2);
+#endif
         const int64_t b1 = 2 * pair + 1;
         const bool odd = b1 < a.n_blocks;  // the pair's second block exists
         const bool emit = pair >= p0;     // pair p0 - 1 only supplies fprev
@@ -1309,6 +1372,8 @@ __global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
             }
         }
     }
+    CONV_PROF_MARK(3);
+    CONV_PROF_FLUSH(2);
 }
 
 int ilog2(int64_t v) {
@@ -1571,6 +1636,17 @@ static void mr_dispatch(const ConvPlan* p, Fn&& fn) {
             fn(std::false_type{}, integral_constant<int, 512>{}, integral_constant<int, 0>{}, integral_constant<int, 0>{});
     }
 }
+
+#if ARX_CONV_PROF
+// Measurement builds only: read (and clear) the per-workgroup phase records (tools/conv_phases.py).
+extern "C" int arx_exp_conv_profile(unsigned long long* out, size_t n_words) {
+    const size_t total = 3 * (size_t)kProfPass;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_conv_prof), std::min(n_words, total) * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    std::vector<unsigned long long> z(total, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_conv_prof), z.data(), total * 8, 0, hipMemcpyHostToDevice) != hipSuccess;
+}
+#endif
 
 hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
     (void)hipGetLastError();  // report this launch's error, not a stale one
