@@ -41,3 +41,9 @@ def conference():
     from audiorenderingv2_amd.scene import conference_standin
 
     return conference_standin()
+
+
+def pytest_unconfigure(config):
+    # marks the end of the session in GPU logs: anything after it (a crash at interpreter exit) is
+    # teardown, not a test
+    print("\n[conftest] pytest session unconfigured", flush=True)

@@ -6,7 +6,7 @@
 // history at commit 62a5de6.)
 //
 //   g++ -O2 -std=c++17 -I audiorenderingv2_amd/csrc tools/bvh_stats.cpp \
-//       audiorenderingv2_amd/csrc/arx_bvh.cpp -o /tmp/bvh_stats
+//       audiorenderingv2_amd/csrc/arx_bvh.cpp oracle/liboracle.so -o /tmp/bvh_stats
 //   /tmp/bvh_stats scene.f32 n_tris ex ey ez n_rays bounces
 // (The insertion-based optimisation tried in round 4 -- REINSERT / RESEG -- is at commit 198ae4a.)
 #include <algorithm>
@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "arx_bvh.hpp"
+extern "C" void orc_ray_direction(uint64_t seed, uint64_t ray_id, float dir[3]);  // oracle/arx_oracle.c (CHAINS=1)
 
 using namespace arx;
 
@@ -200,10 +201,16 @@ int main(int argc, char** argv) {
         Stats st;
         long queries = 0;
         std::mt19937 r2(7);
+        // per-ray node visits (CHAINS=1: the launch's rays in order, directions from the oracle's
+        // Philox stream, seed 1): the lane chains of the small-launch trace (one ray per lane)
+        static const bool chains = std::getenv("CHAINS") != nullptr;
+        std::vector<double> ray_visits;
         for (int i = 0; i < nr; ++i) {
             const float z = 2 * U(r2) - 1, ph = 6.2831853f * U(r2), s = std::sqrt(1 - z * z);
             Q q;
             float o[3] = {em[0], em[1], em[2]}, d[3] = {s * std::cos(ph), s * std::sin(ph), z};
+            if (chains) orc_ray_direction(1, (uint64_t)i, d);
+            const double v_before = st.visits + st.leaves;
             for (int bn = 0; bn < nb; ++bn) {
                 for (int a = 0; a < 3; ++a) {
                     q.o[a] = o[a];
@@ -227,6 +234,26 @@ int main(int argc, char** argv) {
                     o[a] += 1e-3f * d[a];
                 }
             }
+            if (chains) ray_visits.push_back(st.visits + st.leaves - v_before);
+        }
+        if (chains && !ray_visits.empty()) {
+            // waves of 64 consecutive rays (the small launch's static ranges): a wave's lanes step
+            // in lockstep, so its chain is at least its longest lane's
+            std::vector<double> wave_max;
+            for (size_t w = 0; w < ray_visits.size(); w += 64)
+                wave_max.push_back(*std::max_element(ray_visits.begin() + w,
+                                                     ray_visits.begin() + std::min(ray_visits.size(), w + 64)));
+            std::vector<double> sv = ray_visits;
+            std::sort(sv.begin(), sv.end());
+            std::sort(wave_max.begin(), wave_max.end());
+            double mean = 0;
+            for (double v : sv) mean += v;
+            mean /= sv.size();
+            std::printf("per-ray node steps + leaf visits: mean %.1f p50 %.0f p99 %.0f p99.9 %.0f max %.0f\n", mean,
+                        sv[sv.size() / 2], sv[sv.size() * 99 / 100], sv[sv.size() * 999 / 1000], sv.back());
+            std::printf("per-wave (64 rays) longest lane: mean %.1f p50 %.0f max %.0f\n",
+                        [&] { double m = 0; for (double v : wave_max) m += v; return m / wave_max.size(); }(),
+                        wave_max[wave_max.size() / 2], wave_max.back());
         }
         const double v = st.visits / queries, te = st.tests / queries, lv = st.leaves / queries;
         std::printf("W=%d: %ld queries  visits %.1f  leaves %.1f  tri tests %.1f  node bytes %.0f  tri bytes %.0f  "
