@@ -7,10 +7,12 @@ call goes through libarx.so's C ABI (include/arx.h); there is no CPU fallback.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import dataclasses
 import os
 import time
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -18,6 +20,22 @@ import numpy as np
 from ._lib import ArxConfig, ArxStats, check, fptr, lib
 from .formats import write_float_lines
 from .scene import Scene
+
+# Every live native object, released at interpreter exit (streams, then buffers, groups and
+# renderers), while the HIP and RCCL runtimes are still whole: objects the interpreter would finalize
+# only during its own teardown -- or never -- otherwise reach the runtimes' exit-time destructors
+# still allocated (a double free inside HIP 7.2's teardown was the result).
+_LIVE: "dict[str, weakref.WeakSet]" = {k: weakref.WeakSet() for k in ("stream", "buffer", "group", "renderer")}
+
+
+@atexit.register
+def _release_all() -> None:
+    for kind in ("stream", "buffer", "group", "renderer"):
+        for obj in list(_LIVE[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
 
 
 @dataclass
@@ -61,6 +79,7 @@ class AudioRenderer:
         else:
             cfg = settings.to_c()
             check(lib().arx_create(C.byref(cfg), C.byref(self._h)))
+            _LIVE["renderer"].add(self)
         self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
         if receiver is not None:
             self.set_receiver_model(*receiver)
@@ -305,6 +324,7 @@ class LiveStream:
         self.renderer = renderer
         self._s = C.c_void_p()
         check(lib().arx_stream_create(renderer.handle, int(block_frames), C.byref(self._s)))
+        _LIVE["stream"].add(self)
         b, p, n = C.c_int32(), C.c_int32(), C.c_int32()
         check(lib().arx_stream_info(self._s, C.byref(b), C.byref(p), C.byref(n)))
         self.block_frames, self.partitions, self.fft_size = b.value, p.value, n.value
@@ -357,6 +377,7 @@ class RenderGroup:
             devs = list(devices if devices is not None else [settings.device])
             arr = (C.c_int32 * len(devs))(*devs)
             check(lib().arx_group_create(C.byref(cfg), arr, len(devs), C.byref(self._g)))
+        _LIVE["group"].add(self)
         self.ir_length = settings.ir_length_in_seconds * settings.sample_rate
         self.members = []
         for i in range(lib().arx_group_members(self._g)):
@@ -480,6 +501,7 @@ class DeviceBuffer:
         p = C.c_void_p()
         check(lib().arx_device_alloc(self.device, self.nbytes, C.byref(p)))
         self.ptr = int(p.value)
+        _LIVE["buffer"].add(self)
 
     @classmethod
     def from_numpy(cls, device: int, a: np.ndarray) -> "DeviceBuffer":
