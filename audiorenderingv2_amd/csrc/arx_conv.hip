@@ -1411,7 +1411,7 @@ __global__ __launch_bounds__(512) void pass_c_mr(MrArgs m) {
 // (column, row) one step earlier and holds in registers.  Sums in pass D's order (0 + F + E),
 // rounded once; no block window goes through HBM (Y), and no seam pass runs.
 template <bool R7, int LM, int L1>
-__global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
+__device__ __forceinline__ void pass_c_chain_body(const MrArgs& m) {
     constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
@@ -1505,6 +1505,18 @@ __global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
     }
     CONV_PROF_MARK(3);
     CONV_PROF_FLUSH(2);
+}
+// The compile-time plans (L1 > 0) fit in 168 VGPRs = 3 waves per SIMD without spilling; left to
+// itself the compiler took 169 (2 waves), so the C3 launch's 640 four-wave blocks (2.5 waves per
+// SIMD) ran in two rounds (8.5 us entry skew, tools/conv_phases.py).  The run-time plans keep the
+// unconstrained allocation (168 would spill there).
+template <bool R7, int LM, int L1>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(3))) void pass_c_chain3(MrArgs m) {
+    pass_c_chain_body<R7, LM, L1>(m);
+}
+template <bool R7, int LM, int L1>
+__global__ __launch_bounds__(512) void pass_c_chain(MrArgs m) {
+    pass_c_chain_body<R7, LM, L1>(m);
 }
 
 int ilog2(int64_t v) {
@@ -1732,8 +1744,12 @@ static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool wi
     if (p->n == 2 * p->sr && p->N1 % 2 == 0) {  // inverse columns and seams in one pass
         m.chain = ARX_CONV_CHAIN;
         const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
-        hipLaunchKernelGGL((pass_c_chain<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains), dim3(64 * ARX_CONV_TCC),
-                           mr_lds_c(p, ARX_CONV_TCC), s, m);
+        if constexpr (L1 > 0)
+            hipLaunchKernelGGL((pass_c_chain3<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains),
+                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
+        else
+            hipLaunchKernelGGL((pass_c_chain<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains),
+                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
         return;
     }
     hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), (unsigned)(2 * pairs)),

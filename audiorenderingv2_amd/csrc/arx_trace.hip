@@ -1059,6 +1059,16 @@ constexpr int kSmallSteps = ARX_TRACE_SMALL_STEPS, kSmallLeaf = ARX_TRACE_SMALL_
 #endif
 constexpr bool kSmallFuse = ARX_TRACE_FUSE_SMALL != 0;
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
+// ... rays per wave (fewer than 64: more, sparser waves up to the persistent grid's capacity) and the
+// shading threshold there
+#ifndef ARX_TRACE_SMALL_RPW
+#define ARX_TRACE_SMALL_RPW 64
+#endif
+#ifndef ARX_TRACE_SMALL_THRESH
+#define ARX_TRACE_SMALL_THRESH ARX_TRACE_THRESH
+#endif
+constexpr int kSmallRaysPerWave = ARX_TRACE_SMALL_RPW, kSmallThresh = ARX_TRACE_SMALL_THRESH;
+static_assert(kSmallRaysPerWave >= 1 && kSmallRaysPerWave <= 64, "rays per wave of a small launch: 1..64");
 constexpr int kSimdsPerCu = 4;
 
 // Persistent grid of BLOCK-lane blocks: exactly kWaves waves per SIMD on every CU, fewer blocks
@@ -1101,8 +1111,8 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
         // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
         constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
-        const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, n_rays);
-        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK, kSmallFuse>), dim3(g2),
+        const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, (n_rays * 64 + kSmallRaysPerWave - 1) / kSmallRaysPerWave);
+        hipLaunchKernelGGL((trace_kernel<SB, kSmallThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK, kSmallFuse>), dim3(g2),
                            dim3(SB), dyn_lds, s, a2);
     } else {
         hipLaunchKernelGGL((trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(grid),
@@ -1141,20 +1151,20 @@ bool trace_uses_small_block(const TraceArgs& a, int cus, bool force_global_stack
 }
 
 namespace {
-template <int B, int L, int S>
+template <int B, int T, int L, int S>
 const void* lds_stack_instance(int fmt) {
     constexpr bool F = B != kBlock && kSmallFuse;  // the small-launch instance's fusion
-    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtW4, false, F>)
-           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtQ16, false, F>)
-                            : reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtF32, false, F>);
+    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtW4, false, F>)
+           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtQ16, false, F>)
+                            : reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtF32, false, F>);
 }
 }  // namespace
 
 hipError_t trace_kernel_occupancy(int fmt, bool small, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;
     constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
-    const void* k = small ? lds_stack_instance<SB, kSmallLeaf, kSmallSteps>(fmt)
-                          : lds_stack_instance<kBlock, kLeafThresh, kSteps>(fmt);
+    const void* k = small ? lds_stack_instance<SB, kSmallThresh, kSmallLeaf, kSmallSteps>(fmt)
+                          : lds_stack_instance<kBlock, kThresh, kLeafThresh, kSteps>(fmt);
     const hipError_t e = hipFuncGetAttributes(&fa, k);
     if (e != hipSuccess) return e;
     // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8
