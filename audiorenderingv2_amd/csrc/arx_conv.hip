@@ -1225,137 +1225,6 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     CONV_PROF_FLUSH(1);
 }
 
-// Pass B over BM consecutive block pairs per workgroup (design experiment, ARX_CONV_BM > 1): the IR's
-// row FFT and its split into H_L / H_R run once per workgroup instead of once per pair; each further
-// pair costs one forward row FFT (its row prefetched during the previous pair) and the two inverse
-// ones.  Same arithmetic per element as pass_b_pair, so the same results bit for bit.
-template <bool R7, int LM, int L2, int BM>
-__global__ __launch_bounds__(128) void pass_b_multi(MrArgs m) {
-    constexpr int IT = LM / 64;
-    extern __shared__ __attribute__((aligned(16))) double2 lds[];
-    const PassArgs& a = m.p;
-    const int N1 = a.N1, N2 = a.N2, units = (N1 + 1) / 2;
-    const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
-    const int groups = (int)((m.batches + BM - 1) / BM);
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int u = (slot / groups) * 8 + xcd;
-    const int64_t b0 = (int64_t)(slot % groups) * BM;
-    const int64_t b1 = b0 + BM < m.batches ? b0 + BM : m.batches;
-    if (u >= units) return;  // the whole block: no barrier is reached
-    CONV_PROF_DECL
-    CONV_PROF_MARK(0);
-    const bool self = u == 0;
-    const int k1 = w == 0 ? u : (self ? N1 / 2 : N1 - u);
-    const bool live = !(self && w == 1 && (N1 & 1));
-    double2* spec = lds + (size_t)w * 2 * N2;
-    double2* gbuf = spec + N2;
-    double2* gmir = self ? gbuf : lds + (size_t)(w ^ 1) * 2 * N2 + N2;
-    double2* tw2 = lds + (size_t)4 * N2;
-    double2 v[IT], g[IT], twq[IT], twr[IT];
-    const int step = 64 * k1, dq = step / N2, dr = step - dq * N2;
-    int q = (j * k1) / N2, r = j * k1 - q * N2;
-    auto load_row = [&](int64_t batch) {
-        const double2* row = a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            v[it] = (live && i < N2) ? row[i] : make_double2(0.0, 0.0);
-        }
-    };
-    load_row(b0);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int i = j + 64 * it;
-        const bool in = live && i < N2;
-        g[it] = in ? a.G[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
-        twq[it] = in ? a.tw[(int64_t)q * N2] : make_double2(1.0, 0.0);
-        twr[it] = in ? a.tw[r] : make_double2(1.0, 0.0);
-        q += dq;
-        r += dr;
-        if (r >= N2) {
-            r -= N2;
-            ++q;
-        }
-    }
-    stage_table<IT>(tw2, a.tw, N2, N1, 128);
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int i = j + 64 * it;
-        if (i < N2) {
-            spec[i] = v[it];
-            gbuf[i] = g[it];
-        }
-    }
-    __syncthreads();
-    CONV_PROF_MARK(1);
-    fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
-    __syncthreads();  // the mirror row's G spectrum is complete
-    double2 h0[IT], h1[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int i = j + 64 * it;
-        if (i < N2) {
-            const int mi = k1 == 0 ? (i == 0 ? 0 : N2 - i) : N2 - 1 - i;
-            const double2 x = gbuf[i], y = gmir[mi];
-            h0[it] = make_double2(0.5 * (x.x + y.x), 0.5 * (x.y - y.y));
-            h1[it] = make_double2(0.5 * (x.y + y.y), -0.5 * (x.x - y.x));
-        } else {
-            h0[it] = h1[it] = make_double2(0.0, 0.0);
-        }
-    }
-    if (b0 == 0 && live) {
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            if (i < N2) {
-                a.H[(int64_t)k1 * N2 + i] = h0[it];
-                a.H[(size_t)a.M + (int64_t)k1 * N2 + i] = h1[it];
-            }
-        }
-    }
-    __syncthreads();  // every mirror read is done before gbuf is overwritten
-    CONV_PROF_MARK(2);
-    if (!live) return;  // no block-wide barrier below
-    for (int64_t batch = b0; batch < b1; ++batch) {
-        if (batch > b0) {  // this pair's row (loaded during the previous pair), forward
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                const int i = j + 64 * it;
-                if (i < N2) spec[i] = v[it];
-            }
-            __builtin_amdgcn_wave_barrier();
-            fft_wave_any<R7, LM, L2>(spec, tw2, m.f2, j, -1);
-        }
-        if (batch + 1 < b1) load_row(batch + 1);  // in flight during this pair's products and inverses
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            if (i < N2) {
-                const double2 x = spec[i];
-                gbuf[i] = cmul(x, h0[it]);
-                spec[i] = cmul(x, h1[it]);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        fft2_wave_any<R7, LM, L2>(gbuf, spec, tw2, m.f2, j, +1);
-        double2* dst0 = a.S + ((size_t)batch * 3 + 1) * a.M + (int64_t)k1 * N2;
-        double2* dst1 = dst0 + a.M;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = j + 64 * it;
-            if (i < N2) {
-                const double2 tw = cmul(twq[it], twr[it]);
-                const double2 t = make_double2(tw.x, -tw.y);
-                dst0[i] = cmul(gbuf[i], t);
-                dst1[i] = cmul(spec[i], t);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // the next pair rewrites spec / gbuf
-    }
-    CONV_PROF_MARK(3);
-    CONV_PROF_FLUSH(1);
-}
-
 // Pass C: inverse column FFTs of each (pair, channel) -> n * circular convolution of the pair's two
 // blocks (re / im), to Y (length n per block and channel).  LDS: tile tc x sc, W_N1 (N1).
 template <bool R7, int LM, int L1>
@@ -1686,18 +1555,10 @@ static size_t mr_lds_a(const ConvPlan* p, int tc) {
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
-#ifndef ARX_CONV_BM
-#define ARX_CONV_BM 1  // block pairs per pass-B workgroup (design experiments: pass_b_multi)
-#endif
 template <bool R7, int LM, int L2>
 static void launch_b_pair(const ConvPlan* p, int batches, MrArgs m, hipStream_t s) {
     const unsigned units8 = (unsigned)((p->N1 + 1) / 2 + 7) / 8 * 8;  // see pass_b_pair's XCD mapping
     m.batches = batches;
-    if constexpr (ARX_CONV_BM > 1) {
-        const unsigned groups = (unsigned)((batches + ARX_CONV_BM - 1) / ARX_CONV_BM);
-        hipLaunchKernelGGL((pass_b_multi<R7, LM, L2, ARX_CONV_BM>), dim3(units8 * groups), dim3(128), mr_lds_b(p, 2), s, m);
-        return;
-    }
     hipLaunchKernelGGL((pass_b_pair<R7, LM, L2>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2), s, m);
 }
 template <int MODE, bool R7, int LM, int L2>

@@ -679,28 +679,6 @@ __device__ __forceinline__ void leaf_step(__amdgpu_buffer_rsrc_t trs, const Ray&
     }
 }
 
-// Latency-bound launches (about a ray per lane): one slot serves every lane.  Lanes at an inner node
-// take a node step and lanes holding a leaf test it, in the same step: both fetches are issued before
-// either result is used, so the slot costs one memory latency, and no lane waits for a leaf batch
-// while others step.  Lanes at neither load past the buffer ranges (zeros, no access) and keep their
-// state; node_step's push lands above a leaf lane's stack top (free), so both may run for all lanes.
-template <int FMT, typename Stack>
-__device__ __forceinline__ void fused_step(__amdgpu_buffer_rsrc_t trs, const Ray& r, float oix, float oiy, float oiz,
-                                           Trav& t, const Stack& stk, __amdgpu_buffer_rsrc_t nrs,
-                                           const uint4* __restrict__ ncache) {
-    const bool at_node = t.node >= 0;
-    Trav tn = t, tl = t;
-    // a finished lane's sp is -1 (the sentinel pop): its dummy push and pop read must stay off the
-    // sentinel row (LDS) / the column's start (global stack)
-    tn.sp = max(t.sp, 0);
-    tl.sp = tn.sp;
-    node_step<FMT>(r, oix, oiy, oiz, tn, stk, nrs, ncache);
-    leaf_step<FMT>(trs, r, tl, stk);
-    t.best = tl.best;  // a node step leaves the closest hit alone; a leaf step changes it for leaf lanes only
-    t.node = at_node ? tn.node : tl.node;
-    t.sp = at_node ? tn.sp : tl.sp;
-}
-
 // Highest VGPR the trace kernel claims, so that its allocation (granule 8) admits exactly
 // ARX_TRACE_WAVES waves per SIMD: 5 -> 88 VGPRs (512/88 = 5.8), 4 -> 104, 6 -> 80.  Every wave of
 // a persistent launch owns an equal share of the rays, so a SIMD holding one wave more than the
@@ -745,7 +723,7 @@ constexpr int kDynShare = ARX_TRACE_DYN_SHARE, kDynChunk = ARX_TRACE_DYN_CHUNK, 
 // loop: NSTEPS guarded node steps per iteration; leaves are postponed and intersected wave-wide
 // once LEAF_THRESH lanes hold one (or no lane can step); the loop is left when THRESH lanes wait
 // for shading.
-template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT, bool GSTACK, bool FUSE = false>
+template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT, bool GSTACK>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     constexpr bool Q16 = FMT == kFmtQ16;
     constexpr bool W4 = FMT == kFmtW4;
@@ -909,24 +887,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
 #if ARX_TRACE_PROF
             ++pf[11];
 #endif
-            if constexpr (FUSE && !W4) {  // small launches: node and leaf lanes step together
-#pragma unroll
-                for (int k = 0; k < NSTEPS; ++k) {
-#if ARX_TRACE_PROF
-                    const unsigned long long mk = __ballot(t.node >= 0);
-                    if (mk) {
-                        ++pf[4];
-                        pf[5] += __popcll(mk);
-                    }
-#endif
-#if ARX_TRACE_COUNT
-                    if (t.node >= 0) ++n_steps;
-                    if (t.node <= -2) n_tris += (uint32_t)min((~t.node) & 15, 2);
-#endif
-                    if (__ballot(t.node <= -2) != 0ull) fused_step<FMT>(trs, r, oix, oiy, oiz, t, stk, nrs, ncache);
-                    else if (t.node >= 0) node_step<FMT>(r, oix, oiy, oiz, t, stk, nrs, ncache);
-                }
-            } else if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+            if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
 #pragma unroll
                 for (int k = 0; k < NSTEPS; ++k) {
 #if ARX_TRACE_PROF
@@ -1053,22 +1014,7 @@ constexpr int kSmallBlock = ARX_TRACE_SMALL_BLOCK;
 #define ARX_TRACE_SMALL_LEAF 8
 #endif
 constexpr int kSmallSteps = ARX_TRACE_SMALL_STEPS, kSmallLeaf = ARX_TRACE_SMALL_LEAF;
-// ... and whether node and leaf lanes step together there (fused_step)
-#ifndef ARX_TRACE_FUSE_SMALL
-#define ARX_TRACE_FUSE_SMALL 0
-#endif
-constexpr bool kSmallFuse = ARX_TRACE_FUSE_SMALL != 0;
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
-// ... rays per wave (fewer than 64: more, sparser waves up to the persistent grid's capacity) and the
-// shading threshold there
-#ifndef ARX_TRACE_SMALL_RPW
-#define ARX_TRACE_SMALL_RPW 64
-#endif
-#ifndef ARX_TRACE_SMALL_THRESH
-#define ARX_TRACE_SMALL_THRESH ARX_TRACE_THRESH
-#endif
-constexpr int kSmallRaysPerWave = ARX_TRACE_SMALL_RPW, kSmallThresh = ARX_TRACE_SMALL_THRESH;
-static_assert(kSmallRaysPerWave >= 1 && kSmallRaysPerWave <= 64, "rays per wave of a small launch: 1..64");
 constexpr int kSimdsPerCu = 4;
 
 // Persistent grid of BLOCK-lane blocks: exactly kWaves waves per SIMD on every CU, fewer blocks
@@ -1111,9 +1057,9 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
         // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
         constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
-        const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, (n_rays * 64 + kSmallRaysPerWave - 1) / kSmallRaysPerWave);
-        hipLaunchKernelGGL((trace_kernel<SB, kSmallThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK, kSmallFuse>), dim3(g2),
-                           dim3(SB), dyn_lds, s, a2);
+        const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, n_rays);
+        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK>), dim3(g2), dim3(SB),
+                           dyn_lds, s, a2);
     } else {
         hipLaunchKernelGGL((trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(grid),
                            dim3(kBlock), dyn_lds, s, a2);
@@ -1151,20 +1097,19 @@ bool trace_uses_small_block(const TraceArgs& a, int cus, bool force_global_stack
 }
 
 namespace {
-template <int B, int T, int L, int S>
+template <int B, int L, int S>
 const void* lds_stack_instance(int fmt) {
-    constexpr bool F = B != kBlock && kSmallFuse;  // the small-launch instance's fusion
-    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtW4, false, F>)
-           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtQ16, false, F>)
-                            : reinterpret_cast<const void*>(trace_kernel<B, T, L, kWaves, S, kFmtF32, false, F>);
+    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtW4, false>)
+           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtQ16, false>)
+                            : reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtF32, false>);
 }
 }  // namespace
 
 hipError_t trace_kernel_occupancy(int fmt, bool small, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;
     constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
-    const void* k = small ? lds_stack_instance<SB, kSmallThresh, kSmallLeaf, kSmallSteps>(fmt)
-                          : lds_stack_instance<kBlock, kThresh, kLeafThresh, kSteps>(fmt);
+    const void* k = small ? lds_stack_instance<SB, kSmallLeaf, kSmallSteps>(fmt)
+                          : lds_stack_instance<kBlock, kLeafThresh, kSteps>(fmt);
     const hipError_t e = hipFuncGetAttributes(&fa, k);
     if (e != hipSuccess) return e;
     // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8

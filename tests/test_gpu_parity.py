@@ -417,7 +417,11 @@ def test_convolution_c3_size_with_rendered_ir(conference):
 
 
 def test_convolution_device_api_equals_host_api():
-    torch = pytest.importorskip("torch")
+    # device buffers of the package itself (arx_device_alloc), not another framework's: a second HIP
+    # runtime in the process (torch's) also loads libamd_smi, whose globals interpose librocm_smi64's
+    # (RCCL's) and are then destroyed twice at interpreter exit (double free, the whole suite aborts)
+    from audiorenderingv2_amd import DeviceBuffer
+
     sr = 16000
     rng = np.random.default_rng(3)
     r = conv_renderer(sr)
@@ -425,14 +429,14 @@ def test_convolution_device_api_equals_host_api():
     r.set_ir(irl, irr)
     x = rng.standard_normal(5 * sr + 17).astype(np.float32)
     L, R, _, _ = r.convoluteAudioFile(x)
-    dx = torch.from_numpy(x).cuda()
-    dl = torch.empty_like(dx)
-    dr = torch.empty_like(dx)
-    torch.cuda.synchronize()
-    r.convolute_device(dx.data_ptr(), x.size, dl.data_ptr(), dr.data_ptr())
+    dx = DeviceBuffer.from_numpy(0, x)
+    dl, dr = DeviceBuffer(0, x.nbytes), DeviceBuffer(0, x.nbytes)
+    r.convolute_device(dx.ptr, x.size, dl.ptr, dr.ptr)
     import audiorenderingv2_amd._lib as L_
     L_.check(L_.lib().arx_copy_ir(r.handle, None, None, r.ir_length))  # syncs the renderer stream
-    assert np.array_equal(dl.cpu().numpy(), L) and np.array_equal(dr.cpu().numpy(), R)
+    assert np.array_equal(dl.to_numpy(np.float32, x.size), L) and np.array_equal(dr.to_numpy(np.float32, x.size), R)
+    for b in (dx, dl, dr):
+        b.close()
     # one timing pair per convolution, host and device entry points alike (arx_conv_times)
     t = r.conv_times(8)
     assert len(t) == 2 and np.all(t > 0)
