@@ -43,6 +43,18 @@ def conference():
     return conference_standin()
 
 
+@pytest.fixture(autouse=True)
+def _no_second_hip_runtime(request):
+    """GPU tests must not bring another GPU framework into the test process: torch's bundled HIP
+    runtime loads libamd_smi, whose global tables interpose those of RCCL's librocm_smi64; both
+    libraries then destroy the same objects at interpreter exit and the process aborts (double
+    free) after every test has passed (profiles/r04/exit_abort_backtrace.txt).  Device memory for a
+    test comes from audiorenderingv2_amd.DeviceBuffer; torch runs only in subprocesses."""
+    yield
+    if request.node.get_closest_marker("gpu") is not None:
+        assert "torch" not in sys.modules, f"{request.node.nodeid} imported torch into the GPU test process"
+
+
 def pytest_unconfigure(config):
     # marks the end of the session in GPU logs: anything after it (a crash at interpreter exit) is
     # teardown, not a test

@@ -462,7 +462,6 @@ def test_rejects_absorption_and_hrtf_outside_unit_interval():
 def test_set_ir_device_equals_set_ir():
     """arx_set_ir_device: another renderer's IR taken by a device copy convolves like the same IR
     set from the host."""
-    torch = pytest.importorskip("torch")
     sr = 16000
     rng = np.random.default_rng(11)
     a, b = conv_renderer(sr), conv_renderer(sr)
