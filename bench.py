@@ -573,7 +573,7 @@ def main(argv=None) -> int:
                                        ("workload", "tree_hash", "trace_kernel_id"))
     td, td_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_td_c3.json")), args.workload, st0)
     vmem, vmem_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_vmem_ceiling.json")), args.workload, st0)
-    conv_traffic = load_profile(os.path.join("r02", "conv_traffic_r02m.json"))
+    conv_traffic = load_profile(os.path.join(PROFILES, "conv_traffic_r04j.json"))
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)
     result = {
         "metric": METRIC,
@@ -640,7 +640,7 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
             "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and args.workload == "c3" else None,
             "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and args.workload == "c3" else None,
-            "traffic_source": "profiles/r02/conv_traffic_r02m.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
+            "traffic_source": f"profiles/{PROFILES}/conv_traffic_r04j.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
                               "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
