@@ -424,6 +424,10 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--preroll-s", type=float, default=0.5,
+                    help="untimed steps for this long before the warmup steps: a fresh process on an idle GPU "
+                         "runs its first ~10 C3 launches 2.95 -> 2.67 ms while the clock ramps, and again after "
+                         "2 s idle (tools/trace_ramp.py, profiles/r04/trace_ramp.json)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -501,6 +505,17 @@ def main(argv=None) -> int:
         for m, (x, ol, orr) in zip(members, bufs):
             m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
+    # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
+    # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
+    # same number of steps and their all-reduces stay paired.
+    t_pre, pre_steps = time.perf_counter(), 0
+    while True:
+        step()
+        g.synchronize()
+        pre_steps += 1
+        if ranks.max(1.0 if time.perf_counter() - t_pre < args.preroll_s else 0.0) == 0.0:
+            break
+    preroll_s = time.perf_counter() - t_pre
     for _ in range(args.warmup):
         step()
     g.synchronize()
@@ -604,6 +619,10 @@ def main(argv=None) -> int:
         },
         "runtime": runtime_info(),
         "setup_s_rank0": setup_s,
+        "preroll": {"steps": pre_steps, "seconds_rank0": preroll_s,
+                    "why": "untimed steps before the W warmup steps, until the GPU runs at its sustained clock "
+                           "(a fresh or idle MI355X ramps over its first ~10 C3 launches, 2.95 -> 2.67 ms; "
+                           "profiles/r04/trace_ramp.json)"},
         "ray_bounces_per_step": q_all,
         "nominal_ray_bounces_per_s": total_rays * wl["max_bounces"] * args.steps / elapsed,
         "receiver_hits_per_step_rank0": int(st0["receiver_hits"]),
