@@ -252,6 +252,12 @@ arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris) {
 
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_img) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
+    if (r->scene_dirty || r->recv_model_dirty || r->recv_pose_dirty || !r->qgrid_set) {
+        // the uploads, re-quantization and receiver refit below write the tree the other frame in
+        // flight may still be tracing
+        const arx_status st = fif_wait_traced(r);
+        if (st != ARX_OK) return st;
+    }
     const SceneImage& img = *r->scene_img;
     const BvhBuild& sc = img.bvh;
     const bool model_changed = r->recv_model_dirty || r->scene_dirty;
@@ -511,7 +517,7 @@ struct arx_stream {
 namespace {
 void release_stream(arx_stream* s) {
     hipSetDevice(s->device);
-    if (s->r && s->r->stream) hipStreamSynchronize(s->r->stream);
+    if (s->r) sync_renderer(s->r);
     if (s->plan) stream_plan_destroy(s->plan);
     hipFree(s->d_in);
     hipFree(s->d_out);
@@ -874,6 +880,42 @@ float arx_material_absorption(const char* name, const char* const* names, const 
     return 0.5f;
 }
 
+}  // extern "C"
+
+namespace {
+void free_frame_set(arx_renderer::FrameSet& f) {
+    if (f.stream) hipStreamDestroy(f.stream);
+    hipFree(f.d_hist);
+    hipFree(f.d_ir);
+    hipFree(f.d_counters);
+    hipFree(f.d_dirs);
+    if (f.h_counters) hipHostFree(f.h_counters);
+    f = arx_renderer::FrameSet{};
+}
+// wait: the current frame set's stream on the other set's event (frames in flight only)
+arx_status fif_wait(arx_renderer* r, hipEvent_t (&ev)[2]) {
+    if (r->fif == 2) ARX_HIP(hipStreamWaitEvent(r->stream, ev[r->slot ^ 1], 0));
+    return ARX_OK;
+}
+arx_status fif_done(arx_renderer* r, hipEvent_t (&ev)[2]) {
+    if (r->fif == 2) ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
+    return ARX_OK;
+}
+}  // namespace
+
+arx_status arx::fif_wait_traced(arx_renderer* r) { return fif_wait(r, r->ev_traced); }
+arx_status arx::fif_wait_conv(arx_renderer* r) { return fif_wait(r, r->ev_conv); }
+arx_status arx::fif_wait_reduced(arx_renderer* r) { return fif_wait(r, r->ev_reduced); }
+arx_status arx::fif_done_reduced(arx_renderer* r) { return fif_done(r, r->ev_reduced); }
+arx_status arx::sync_renderer(arx_renderer* r) {
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (r->stream) ARX_HIP(hipStreamSynchronize(r->stream));
+    if (r->alt.stream) ARX_HIP(hipStreamSynchronize(r->alt.stream));
+    return ARX_OK;
+}
+
+extern "C" {
+
 // The per-launch timing events only time: no system-scope fence when they are recorded (with one,
 // each marker wrote back and invalidated the caches, a few microseconds of stream time per event).
 constexpr unsigned kTimingEvent = hipEventDisableSystemFence;
@@ -938,6 +980,11 @@ void arx_destroy(arx_renderer* r) {
     if (!r) return;
     hipSetDevice(r->cfg.device);
     if (r->stream) hipStreamSynchronize(r->stream);
+    if (r->alt.stream) hipStreamSynchronize(r->alt.stream);
+    free_frame_set(r->alt);
+    for (int k = 0; k < 2; ++k)
+        for (hipEvent_t e : {r->ev_traced[k], r->ev_conv[k], r->ev_reduced[k]})
+            if (e) hipEventDestroy(e);
     for (arx_stream* s : r->streams) release_stream(s);  // the handles stay valid but detached
     r->streams.clear();
     if (r->conv) conv_plan_destroy(r->conv);
@@ -983,6 +1030,7 @@ arx_status arx_get_config(const arx_renderer* r, arx_config* out) {
 
 arx_status arx_set_stream(arx_renderer* r, void* s) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (r->fif != 1) return fail(ARX_ERR_INVALID_ARGUMENT, "a caller's stream needs one frame in flight (arx_set_frames_in_flight)");
     r->stream = (hipStream_t)s;
     return ARX_OK;
 }
@@ -1068,6 +1116,17 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed) {
 arx_status arx_clear_histogram(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     ARX_HIP(hipSetDevice(r->cfg.device));
+    if (r->fif == 2) {  // a frame starts: it takes the other stream, histogram, IR, counters and directions
+        std::swap(r->own_stream, r->alt.stream);
+        r->stream = r->own_stream;
+        std::swap(r->d_hist, r->alt.d_hist);
+        std::swap(r->d_ir, r->alt.d_ir);
+        std::swap(r->d_counters, r->alt.d_counters);
+        std::swap(r->h_counters, r->alt.h_counters);
+        std::swap(r->d_dirs, r->alt.d_dirs);
+        std::swap(r->dirs_cap, r->alt.dirs_cap);
+        r->slot ^= 1;
+    }
     ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
     return ARX_OK;
 }
@@ -1167,7 +1226,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
     ++r->trace_launches;
-    return ARX_OK;
+    return fif_done(r, r->ev_traced);
 }
 
 arx_status arx_finalize_ir(arx_renderer* r) {
@@ -1194,6 +1253,44 @@ arx_status arx_render(arx_renderer* r, double* render_ms) {
     return ARX_OK;
 }
 
+arx_status arx_set_frames_in_flight(arx_renderer* r, int32_t n) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n != 1 && n != 2) return fail(ARX_ERR_INVALID_ARGUMENT, "frames in flight: 1 or 2, not %d", n);
+    if (n == r->fif) return ARX_OK;
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    if (n == 1) {  // the current set stays, the other goes
+        const arx_status st = sync_renderer(r);
+        if (st != ARX_OK) return st;
+        free_frame_set(r->alt);
+        r->fif = 1;
+        return ARX_OK;
+    }
+    if (r->stream != r->own_stream)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own streams (arx_set_stream)");
+    if (r->d_hist_ext) return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own histograms");
+    for (int k = 0; k < 2; ++k)
+        for (hipEvent_t* e : {&r->ev_traced[k], &r->ev_conv[k], &r->ev_reduced[k]})
+            if (!*e) ARX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    arx_renderer::FrameSet f;
+    const size_t bins = 2 * (size_t)r->ir_len;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(&f.d_hist, bins * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc(&f.d_ir, bins * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc(&f.d_counters, (kCursor + 1) * sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipHostMalloc(&f.h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMemsetAsync(f.d_hist, 0, bins * sizeof(unsigned long long), f.stream)) != hipSuccess ||
+        (e = hipMemsetAsync(f.d_ir, 0, bins * sizeof(float), f.stream)) != hipSuccess ||
+        (e = hipMemsetAsync(f.d_counters, 0, (kCursor + 1) * sizeof(unsigned long long), f.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(f.stream)) != hipSuccess) {
+        free_frame_set(f);
+        return fail(ARX_ERR_HIP, "arx_set_frames_in_flight: %s", hipGetErrorString(e));
+    }
+    r->alt = f;
+    r->fif = 2;
+    return ARX_OK;
+}
+
 arx_status arx_histogram_device(arx_renderer* r, int64_t** d_hist, size_t* n) {
     if (!r || !d_hist) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
     *d_hist = (int64_t*)r->hist();
@@ -1205,6 +1302,8 @@ arx_status arx_attach_histogram(arx_renderer* r, int64_t* d_hist, size_t n) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (d_hist && n != 2 * (size_t)r->ir_len)
         return fail(ARX_ERR_INVALID_ARGUMENT, "histogram needs 2*ir_len = %zu elements, got %zu", 2 * (size_t)r->ir_len, n);
+    if (d_hist && r->fif != 1)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "an attached histogram needs one frame in flight (arx_set_frames_in_flight)");
     r->d_hist_ext = (unsigned long long*)d_hist;
     return ARX_OK;
 }
@@ -1319,20 +1418,21 @@ static arx_status ensure_conv_live(arx_renderer* r, int32_t block) {
 arx_status arx_prepare_ir_spectra(arx_renderer* r, int which) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    arx_status st = ARX_OK;
-    if (which & 1) st = ensure_conv(r);
+    arx_status st = fif_wait_conv(r);
+    if (st == ARX_OK && (which & 1)) st = ensure_conv(r);
     if (st == ARX_OK && (which & 2)) st = ensure_conv_live(r, 1);
-    return st;
+    return st == ARX_OK ? fif_done(r, r->ev_conv) : st;
 }
 
 arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len) {
     if (!r || !buf || len == 0) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL renderer or buffer");
     if (which != 1 && which != 2) return fail(ARX_ERR_INVALID_ARGUMENT, "which must be 1 (file) or 2 (live)");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    arx_status st = which == 1 ? ensure_conv(r) : ensure_conv_live(r, 1);
+    arx_status st = fif_wait_conv(r);
+    if (st == ARX_OK) st = which == 1 ? ensure_conv(r) : ensure_conv_live(r, 1);
     if (st != ARX_OK) return st;
     std::snprintf(buf, len, "%s", conv_plan_describe(which == 1 ? r->conv : r->conv_live));
-    return ARX_OK;
+    return fif_done(r, r->ev_conv);
 }
 
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
@@ -1340,7 +1440,9 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (n_frames > 0 && (!d_in || !d_out_left || !d_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    arx_status st = ensure_conv(r, false);
+    // the plan's spectra and scratch, and the caller's outputs, are shared with the other frame in flight
+    arx_status st = fif_wait_conv(r);
+    if (st == ARX_OK) st = ensure_conv(r, false);
     if (st != ARX_OK) return st;
     const bool ir_new = r->conv_ir_dirty;
     const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
@@ -1350,7 +1452,7 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     r->conv_ir_dirty = false;
     ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
     ++r->conv_launches;
-    return ARX_OK;
+    return fif_done(r, r->ev_conv);
 }
 
 arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t in_bytes, float* h_out_left,
@@ -1359,6 +1461,7 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
     const size_t n = in_bytes / sizeof(float);  // AudioRenderer.cpp:689: bytes / sizeof(float)
     if (n > 0 && (!h_in || !h_out_left || !h_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
+    if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the staging buffers below
     hipEvent_t p0, p1;
     ARX_HIP(hipEventCreate(&p0));
     ARX_HIP(hipEventCreate(&p1));
@@ -1402,14 +1505,15 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
         return fail(ARX_ERR_INVALID_ARGUMENT, "live block of %zu samples exceeds ir_len %d", n_in, r->ir_len);
     if ((n_in > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    arx_status st = ensure_conv_live(r, (int32_t)std::max<size_t>(n_in, 1));
+    arx_status st = fif_wait_conv(r);
+    if (st == ARX_OK) st = ensure_conv_live(r, (int32_t)std::max<size_t>(n_in, 1));
     if (st != ARX_OK) return st;
     const int slot = (int)(r->live_launches % arx_renderer::kTraceRing);
     ARX_HIP(hipEventRecord(r->lev0[slot], r->stream));
     ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
     ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
     ++r->live_launches;
-    return ARX_OK;
+    return fif_done(r, r->ev_conv);
 }
 
 arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t in_bytes, double* h_out,
@@ -1422,6 +1526,7 @@ arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t 
     if (n_in > (size_t)r->ir_len)
         return fail(ARX_ERR_INVALID_ARGUMENT, "live block of %zu samples exceeds ir_len %d", n_in, r->ir_len);
     ARX_HIP(hipSetDevice(r->cfg.device));
+    if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the staging buffers below
     if (!r->d_live_in) {
         ARX_HIP(hipMalloc(&r->d_live_in, (size_t)r->ir_len * sizeof(double)));
         ARX_HIP(hipMalloc(&r->d_live_out, 2 * (size_t)r->ir_len * sizeof(double)));
@@ -1534,8 +1639,9 @@ arx_status arx_stream_reset(arx_stream* s) {
     arx_status st = live_stream(s);
     if (st != ARX_OK) return st;
     ARX_HIP(hipSetDevice(s->r->cfg.device));
+    if (const arx_status w = fif_wait_conv(s->r); w != ARX_OK) return w;
     ARX_HIP(stream_reset(s->plan, s->r->stream));
-    return ARX_OK;
+    return fif_done(s->r, s->r->ev_conv);
 }
 
 arx_status arx_stream_info(const arx_stream* s, int32_t* block, int32_t* partitions, int32_t* fft_size) {
@@ -1554,6 +1660,7 @@ arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n
     if ((n_frames > 0 && !d_in) || !d_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     arx_renderer* r = s->r;
     ARX_HIP(hipSetDevice(r->cfg.device));
+    if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the stream's delay line and spectra
     if (s->ir_generation != r->ir_generation) {  // the IR changed: new partition spectra
         ARX_HIP(stream_set_ir(s->plan, r->d_ir, r->d_ir + r->ir_len, r->stream));
         s->ir_generation = r->ir_generation;
@@ -1563,7 +1670,7 @@ arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n
     ARX_HIP(stream_run(s->plan, d_in, (int64_t)n_frames, d_out, r->stream));
     ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
     ++r->live_launches;
-    return ARX_OK;
+    return fif_done(r, r->ev_conv);
 }
 
 arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames, double* h_out, size_t out_len) {
@@ -1574,6 +1681,7 @@ arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames
     if ((n_frames > 0 && !h_in) || !h_out) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     arx_renderer* r = s->r;
     ARX_HIP(hipSetDevice(r->cfg.device));
+    if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the staging buffers below
     if (n_frames > 0)
         ARX_HIP(hipMemcpyAsync(s->d_in, h_in, n_frames * sizeof(double), hipMemcpyHostToDevice, r->stream));
     const arx_status st = arx_stream_process_device(s, s->d_in, n_frames, s->d_out);

@@ -182,10 +182,7 @@ arx_status arx_group_create_rank(const arx_config* cfg, int32_t n_ranks, int32_t
 
 void arx_group_destroy(arx_group* g) {
     if (!g) return;
-    for (arx_renderer* r : g->members) {
-        hipSetDevice(r->cfg.device);
-        hipStreamSynchronize(r->stream);
-    }
+    for (arx_renderer* r : g->members) sync_renderer(r);
     destroy_members(g);
     delete g;
 }
@@ -394,6 +391,12 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
     // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:
     //    its communicator is kept for the group's other collectives, the render skips the no-op)
     if (!g->comms.empty() && g->n_ranks > 1) {
+        // with two frames in flight, each member's all-reduce after its previous one (the
+        // collectives on a communicator keep their order whichever stream they run on)
+        for (arx_renderer* r : g->members) {
+            const arx_status st = fif_wait_reduced(r);
+            if (st != ARX_OK) return st;
+        }
         ARX_NCCL(ncclGroupStart());
         for (size_t i = 0; i < g->members.size(); ++i) {
             arx_renderer* r = g->members[i];
@@ -404,6 +407,10 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
             }
         }
         ARX_NCCL(ncclGroupEnd());
+        for (arx_renderer* r : g->members) {
+            const arx_status st = fif_done_reduced(r);
+            if (st != ARX_OK) return st;
+        }
     } else if (g->device_sum) {
         // Member 0's stream does all of it -- sum the shards into member 0's histogram, then copy the
         // total back into every other member's -- and the others wait for that before finalising.
@@ -444,11 +451,11 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
 }
 
 arx_status arx_group_synchronize(arx_group* g) {
-    return for_all(g, [&](arx_renderer* r) -> arx_status {
-        ARX_HIP(hipSetDevice(r->cfg.device));
-        ARX_HIP(hipStreamSynchronize(r->stream));
-        return ARX_OK;
-    });
+    return for_all(g, [&](arx_renderer* r) { return sync_renderer(r); });
+}
+
+arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_frames_in_flight(r, n); });
 }
 
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len) {
@@ -460,6 +467,10 @@ arx_status arx_group_allreduce_f64(arx_group* g, double* values, size_t n, int o
     if (!g || g->members.empty() || (n > 0 && !values) || (op != 0 && op != 1))
         return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
     if (g->comms.empty() || n == 0 || (int32_t)g->members.size() == g->n_ranks) return ARX_OK;  // one process
+    for (arx_renderer* r : g->members) {  // nothing of a frame in flight left ahead of this collective
+        const arx_status st0 = sync_renderer(r);
+        if (st0 != ARX_OK) return st0;
+    }
     // this process's values enter through member 0; the other local members add the identity
     std::vector<double*> bufs(g->members.size(), nullptr);
     std::vector<double> ident(n, op == 0 ? 0.0 : -HUGE_VAL);

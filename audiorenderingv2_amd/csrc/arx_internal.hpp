@@ -85,6 +85,15 @@ namespace arx {
 arx_status last_trace_ms(arx_renderer* r, bool wait, double* ms);
 // Install a built scene (arx_set_scene's second half): uploaded at the next trace.
 arx_status set_scene_image(arx_renderer* r, SceneRef img);
+// Frames in flight (arx_set_frames_in_flight): the current set's stream waits for the other set's
+// last trace / convolution / all-reduce (no-ops with one frame in flight); `done_*` record the
+// current set's.
+arx_status fif_wait_traced(arx_renderer* r);
+arx_status fif_wait_conv(arx_renderer* r);
+arx_status fif_wait_reduced(arx_renderer* r);
+arx_status fif_done_reduced(arx_renderer* r);
+// Both frame sets' streams synchronised.
+arx_status sync_renderer(arx_renderer* r);
 }  // namespace arx
 
 // One renderer = one device (AudioRenderer, AudioRenderer.h:16-152).
@@ -174,6 +183,27 @@ struct arx_renderer {
     size_t conv_cap = 0;
 
     std::vector<arx_stream*> streams;  // live streaming convolutions of this renderer (arx_stream_create)
+
+    // Frames in flight (arx_set_frames_in_flight): with 2, a frame's start (arx_clear_histogram)
+    // swaps the stream, histogram, IR, counters and direction buffer above with this second set, so
+    // frame k + 1 traces on its own stream while frame k's trace finishes and its IR is convolved.
+    // Frame k + 1 waits only where the two meet: writes to the shared scene / receiver buffers wait
+    // for the other set's last trace (ev_traced), uses of the shared convolution plans (and of the
+    // caller's output buffers) for its last convolution (ev_conv), a group's all-reduce for its last
+    // all-reduce on the same communicator (ev_reduced).  `slot` names the set in the fields above.
+    struct FrameSet {
+        hipStream_t stream = nullptr;
+        unsigned long long* d_hist = nullptr;
+        float* d_ir = nullptr;
+        unsigned long long* d_counters = nullptr;
+        unsigned long long* h_counters = nullptr;
+        void* d_dirs = nullptr;
+        uint64_t dirs_cap = 0;
+    };
+    int32_t fif = 1;
+    int32_t slot = 0;
+    FrameSet alt;
+    hipEvent_t ev_traced[2] = {}, ev_conv[2] = {}, ev_reduced[2] = {};
 
     unsigned long long* d_prof = nullptr;  // per-wave records (profiling builds, ARX_TRACE_PROF)
     size_t prof_words = 0;

@@ -144,6 +144,12 @@ class AudioRenderer:
         """Declared by the reference with an empty body (AudioRenderer.cpp:574-576): a no-op,
         kept so callers of that API keep working (the live path zips L/R on the device)."""
 
+    def set_frames_in_flight(self, n: int) -> None:
+        """1 or 2 (arx_set_frames_in_flight): with 2, consecutive render() calls alternate between
+        two streams and buffers, so a render / convolute loop keeps the GPU full; every getter and
+        convolution refers to the last frame started."""
+        check(lib().arx_set_frames_in_flight(self._h, int(n)))
+
     def set_seed(self, seed: int) -> None:
         check(lib().arx_set_seed(self._h, int(seed)))
 
@@ -457,6 +463,10 @@ class RenderGroup:
 
     def setMonoOutput(self, mono: bool) -> None:
         check(lib().arx_group_set_mono_output(self._g, 1 if mono else 0))
+
+    def set_frames_in_flight(self, n: int) -> None:
+        """arx_group_set_frames_in_flight: AudioRenderer.set_frames_in_flight on every member."""
+        check(lib().arx_group_set_frames_in_flight(self._g, int(n)))
 
     def set_seed(self, seed: int) -> None:
         check(lib().arx_group_set_seed(self._g, int(seed)))

@@ -434,7 +434,11 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
-    ap.add_argument("--no-pipelined", action="store_true", help="skip the two-frames-in-flight leg")
+    ap.add_argument("--frames-in-flight", type=int, choices=(1, 2), default=2,
+                    help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
+                         "with 2, step k+1's trace starts while step k finishes; a single-frame leg is timed too")
+    ap.add_argument("--pipelined", action="store_true", help="also time two renderer groups alternating frames")
+    ap.add_argument("--no-pipelined", action="store_true", help="(default; kept for older scripts)")
     ap.add_argument("--process-group", action="store_true",
                     help="take the one-GPU-per-process (RCCL rank) path even at one rank: a rehearsal of the "
                          "torch.distributed.run path on a one-GPU box")
@@ -505,6 +509,7 @@ def main(argv=None) -> int:
         for m, (x, ol, orr) in zip(members, bufs):
             m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
+    g.set_frames_in_flight(args.frames_in_flight)
     # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
     # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
     # same number of steps and their all-reduces stay paired.
@@ -536,6 +541,27 @@ def main(argv=None) -> int:
     m0 = members[0]
     st0 = m0.stats()
     q_m0 = int(st0["queries"])
+    value = q_all * args.steps / elapsed
+    # With two frames in flight a launch's HIP-event window (on its stream) also holds the time it
+    # queues behind the other frame's kernels, so the per-launch times (phases, rooflines) come from
+    # a single-frame leg: the same group, W + K steps with one frame in flight.
+    single_frame = None
+    if args.frames_in_flight > 1:
+        g.set_frames_in_flight(1)
+        for _ in range(args.warmup):
+            step()
+        g.synchronize()
+        ranks.barrier()
+        t0s = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        g.synchronize()
+        ranks.barrier()
+        el1 = ranks.max(time.perf_counter() - t0s)
+        q1 = int(round(ranks.sum(int(g.stats()["queries"]))))
+        single_frame = {"value": q1 * args.steps / el1, "ms_per_step": el1 / args.steps * 1e3,
+                        "why": "the same steps with one frame in flight; the per-launch kernel times below "
+                               "(phases_ms_rank0, roofline) are this leg's"}
     # the trace kernel's own window (direction pre-pass + trace kernel, HIP events on the
     # renderer's stream) for each of the K timed launches of GPU 0 of this process
     trace_list = m0.trace_times(args.steps)
@@ -549,11 +575,10 @@ def main(argv=None) -> int:
     conv_ms = conv_ms_all[0]
     conv_ms_max = ranks.max(max(conv_ms_all))
 
-    value = q_all * args.steps / elapsed
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
     # frames in flight: a second group beside g
     pipelined = None
-    if not args.no_pipelined:
+    if args.pipelined:
         with _stdout_to_stderr():
             if plan["mode"] == "rank":
                 g2 = RenderGroup.rank(settings, world, rank, uids[1], scene=scene, receiver=receiver)
@@ -612,6 +637,7 @@ def main(argv=None) -> int:
             "sample_rate": wl["sample_rate"],
             "ir_len": ir_len,
             "audio_frames_per_gpu": frames,
+            "frames_in_flight": args.frames_in_flight,
             "parallelism": (f"ray-shard x{world}, native RCCL int64 IR all-reduce (arx_group: "
                             + ("one process, ncclCommInitAll over devices " + ",".join(map(str, plan["devices"]))
                                if plan["mode"] == "local" else f"one process per GPU, ncclCommInitRank, rank {rank}")
@@ -619,6 +645,7 @@ def main(argv=None) -> int:
         },
         "runtime": runtime_info(),
         "setup_s_rank0": setup_s,
+        "single_frame": single_frame,
         "preroll": {"steps": pre_steps, "seconds_rank0": preroll_s,
                     "why": "untimed steps before the W warmup steps, until the GPU runs at its sustained clock "
                            "(a fresh or idle MI355X ramps over its first ~10 C3 launches, 2.95 -> 2.67 ms; "

@@ -147,6 +147,15 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed);
  * N rays, finalize the stereo IR (mono merge = addIRs, kernels.cu:519-527).  render_ms gets the
  * trace kernel's device time (the reference's timed window, :495-518). */
 arx_status arx_render(arx_renderer* r, double* render_ms);
+/* Frames in flight (n = 1 or 2; no reference equivalent -- its render() blocks, AudioRenderer.cpp:
+ * 489-523).  With 2, consecutive render() calls alternate between two streams, histograms and IRs:
+ * frame k + 1 traces while frame k's trace finishes and its IR is convolved, so a render/convolute
+ * loop keeps the GPU full.  Results are those of one frame at a time, bit for bit: every getter,
+ * convolution and IR copy refers to the last frame started, and the two frames meet only where they
+ * share state (scene and receiver uploads wait for the other frame's trace; convolutions, IR
+ * spectra and the caller's output buffers for its convolution).  Not with arx_set_stream or
+ * arx_attach_histogram (ARX_ERR_INVALID_ARGUMENT either way round). */
+arx_status arx_set_frames_in_flight(arx_renderer* r, int32_t n);
 
 /* Building blocks of render() for ray-sharded multi-GPU use (no reference equivalent; the
  * reference is single-GPU).  The histogram is 2*ir_len int64 in device memory: [L | R],
@@ -245,6 +254,9 @@ arx_status arx_group_set_seed(arx_group* g, uint64_t seed);
  * (async on the members' streams).  render_ms (if not NULL; synchronises) = the longest shard's
  * trace kernel time. */
 arx_status arx_group_render(arx_group* g, double* render_ms);
+/* arx_set_frames_in_flight on every member; a member's all-reduce waits for its previous one, so
+ * the collectives on each communicator keep their order. */
+arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n);
 arx_status arx_group_synchronize(arx_group* g);
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
 /* Queries / receiver hits / misses summed over this process's members; times = the longest. */

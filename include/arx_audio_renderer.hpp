@@ -241,6 +241,9 @@ class AudioRenderer {
     void set_hrtf_absorption_rate(float v) { check(arx_group_set_hrtf_absorption_rate(g_, v)); }
     void setBasePower(float v) { check(arx_group_set_base_power(g_, v)); }
     void setMonoOutput(bool v) { check(arx_group_set_mono_output(g_, v ? 1 : 0)); }
+    // Not in the reference: 2 lets a render / convolute loop keep two frames in flight
+    // (arx_set_frames_in_flight; results bit-identical to one frame at a time)
+    void setFramesInFlight(int n) { check(arx_group_set_frames_in_flight(g_, n)); }
     // :47 -- declared by the reference, body empty (AudioRenderer.cpp:574-576); kept for source
     // compatibility, it does nothing (the live path zips L/R in pass_d_live)
     void normalizeAndMergeStereoOutput(double*, double*, size_t, double*) {}

@@ -1,0 +1,140 @@
+"""GPU: two frames in flight (arx_set_frames_in_flight) give the results of one frame at a time.
+
+A render / convolute loop on a renderer with two frames in flight alternates two streams, histograms
+and IRs, so frame k + 1 traces while frame k finishes and is convolved.  The frames meet where they
+share state, and these tests drive exactly those places without synchronising between frames:
+  * the listener moves and the emitter moves between frames (the receiver refit and the re-gridding
+    write the tree the previous frame may still be tracing);
+  * the seed changes (other rays) and the convolution plan is shared (IR spectra, scratch);
+  * every frame convolves into the SAME caller buffers as well as into buffers of its own.
+Bar: every frame's convolution, the last IR and the last frame's counters bit-identical to the same
+sequence on a renderer with one frame in flight (itself parity-tested against the oracle in
+test_gpu_parity.py).  The reference renders one frame at a time (AudioRenderer.cpp:489-523).
+"""
+import numpy as np
+import pytest
+
+from audiorenderingv2_amd import ArxError, AudioRenderer, DeviceBuffer, RenderGroup, RenderSettings, receiver_local
+from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER
+
+pytestmark = pytest.mark.gpu
+
+S = dict(rays=(60, 60, 10), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
+# (listener, yaw, emitter, seed) per frame: plain, listener moved and turned, seed changed, emitter
+# moved, listener walked far off the first quantization grid (re-gridding)
+FRAMES = [
+    (CONFERENCE_LISTENER, 0.0, CONFERENCE_EMITTER, 1),
+    ((1.0, 1.2, -0.5), 30.0, CONFERENCE_EMITTER, 1),
+    ((1.0, 1.2, -0.5), 30.0, CONFERENCE_EMITTER, 7),
+    ((1.0, 1.2, -0.5), 30.0, (-4.0, 1.5, 1.0), 7),
+    ((30.0, 1.2, 25.0), 90.0, (-4.0, 1.5, 1.0), 7),
+]
+
+
+def bits(a):
+    return np.asarray(a).view(np.uint32)
+
+
+def run_sequence(obj, members, audio, fif):
+    """The frame loop without a synchronisation between frames; returns per-frame convolutions (own
+    buffers), the shared buffers' final content, the last IR and the last frame's counters."""
+    obj.set_frames_in_flight(fif)
+    n = audio.size
+    x = DeviceBuffer.from_numpy(0, audio)
+    own = [(DeviceBuffer(0, 4 * n), DeviceBuffer(0, 4 * n)) for _ in FRAMES]
+    shared = (DeviceBuffer(0, 4 * n), DeviceBuffer(0, 4 * n))
+    for (lst, yaw, em, seed), (ol, orr) in zip(FRAMES, own):
+        obj.setEmitterPosInOptix(em)
+        obj.setSphereCenterInOptix(lst, yaw)
+        obj.set_seed(seed)
+        if isinstance(obj, RenderGroup):
+            obj.render(timed=False)
+        else:
+            obj.clear_histogram()
+            obj.trace_rays(0, int(np.prod(S["rays"])))
+            obj.finalize_ir()
+        m = members[0]
+        m.convolute_device(x.ptr, n, ol.ptr, orr.ptr)
+        m.convolute_device(x.ptr, n, shared[0].ptr, shared[1].ptr)
+    ir = members[0].get_ir()  # synchronises the last frame
+    st = members[0].stats()
+    outs = [(ol.to_numpy(np.float32), orr.to_numpy(np.float32)) for ol, orr in own]
+    sh = (shared[0].to_numpy(np.float32), shared[1].to_numpy(np.float32))
+    for b in [x, *shared] + [b for pair in own for b in pair]:
+        b.close()
+    return outs, sh, ir, (st["queries"], st["receiver_hits"], st["misses"])
+
+
+@pytest.fixture(scope="module")
+def audio():
+    return (0.5 * np.sin(2 * np.pi * 440 * np.arange(3 * 16000 + 321) / 16000)).astype(np.float32)
+
+
+def test_renderer_two_frames_in_flight_equal_one_at_a_time(conference, audio):
+    res = {}
+    for fif in (1, 2):
+        r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
+        try:
+            res[fif] = run_sequence(r, [r], audio, fif)
+        finally:
+            r.close()
+    (o1, s1, ir1, st1), (o2, s2, ir2, st2) = res[1], res[2]
+    assert ir1[0].any() and st1[1] > 0
+    for k, (a, b) in enumerate(zip(o1, o2)):
+        assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1])), f"frame {k}"
+    # consecutive frames differ, so the comparison above sees each frame's own IR
+    assert not np.array_equal(o1[0][0], o1[1][0]) and not np.array_equal(o1[1][0], o1[2][0])
+    assert np.array_equal(bits(s1[0]), bits(s2[0])) and np.array_equal(bits(s1[1]), bits(s2[1]))
+    assert np.array_equal(bits(s2[0]), bits(o2[-1][0]))  # the shared buffers hold the last frame's
+    assert np.array_equal(bits(ir1[0]), bits(ir2[0])) and np.array_equal(bits(ir1[1]), bits(ir2[1]))
+    assert st1 == st2
+
+
+def test_group_render_two_frames_in_flight_equal_one_at_a_time(conference, audio):
+    res = {}
+    for fif in (1, 2):
+        g = RenderGroup(RenderSettings(**S), devices=[0], scene=conference, receiver=receiver_local())
+        try:
+            res[fif] = run_sequence(g, g.members, audio, fif)
+        finally:
+            g.close()
+    for k, (a, b) in enumerate(zip(res[1][0], res[2][0])):
+        assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1])), f"frame {k}"
+    assert np.array_equal(bits(res[1][2][0]), bits(res[2][2][0])) and res[1][3] == res[2][3]
+
+
+def test_oversubscribed_group_two_frames_in_flight(conference):
+    """Three shards summed on one device (hist_add), two frames in flight: the same IRs."""
+    s = RenderSettings(**S)
+    irs = {}
+    for fif in (1, 2):
+        g = RenderGroup(s, devices=[0, 0, 0], scene=conference, receiver=receiver_local())
+        try:
+            g.set_frames_in_flight(fif)
+            g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+            out = []
+            for lst, yaw, _, seed in FRAMES[:3]:
+                g.setSphereCenterInOptix(lst, yaw)
+                g.set_seed(seed)
+                g.render(timed=False)
+            out.append(g.get_ir())
+            irs[fif] = out
+        finally:
+            g.close()
+    assert np.array_equal(bits(irs[1][0][0]), bits(irs[2][0][0])) and np.array_equal(bits(irs[1][0][1]), bits(irs[2][0][1]))
+
+
+def test_frames_in_flight_refuses_a_callers_stream_or_histogram():
+    r = AudioRenderer(RenderSettings(rays=(4, 4, 4), sample_rate=16000))
+    try:
+        with pytest.raises(ArxError):
+            r.set_frames_in_flight(3)
+        r.set_frames_in_flight(2)
+        with pytest.raises(ArxError):
+            r.set_stream(r.get_stream())
+        with pytest.raises(ArxError):
+            r.attach_histogram(r.histogram_device_ptr()[0], 2 * r.ir_length)
+        r.set_frames_in_flight(1)
+        r.set_stream(r.get_stream())  # allowed again with one frame in flight
+    finally:
+        r.close()

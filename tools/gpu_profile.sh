@@ -10,7 +10,7 @@ O=gpurun_out/${RD:-r04}
 TAG=${TAG:-r04}
 mkdir -p $O
 timeout -k 10 400 python3 bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || { echo "bench failed"; tail -20 $O/bench_$TAG.err; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --c5-frames 0 --no-pipelined --no-streaming > $O/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof_$TAG.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_$TAG -o run -- python3 bench.py --frames-in-flight 1 --no-cpu-baseline --c5-frames 0 --no-streaming > $O/prof_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 $O/prof_$TAG.log; exit 1; }
 mkdir -p $O/pmc_traffic_$TAG
 for grp in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
   ARX_GUARD_OUT=$R/$O/guard_traffic.json timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $R/$O/pmc_traffic_$TAG/$grp -o p -- python3 tools/trace_once.py 2 > $O/pmc_traffic_$TAG/$grp.log 2>&1 || { echo "pmc $grp failed"; tail -5 $O/pmc_traffic_$TAG/$grp.log; exit 1; }
