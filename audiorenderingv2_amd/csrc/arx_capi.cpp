@@ -250,9 +250,20 @@ arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris) {
     return ARX_OK;
 }
 
+// wait: the current frame set's stream on the other set's event (frames in flight only)
+arx_status fif_wait(arx_renderer* r, hipEvent_t (&ev)[2]) {
+    if (r->fif == 2) ARX_HIP(hipStreamWaitEvent(r->stream, ev[r->slot ^ 1], 0));
+    return ARX_OK;
+}
+arx_status fif_done(arx_renderer* r, hipEvent_t (&ev)[2]) {
+    if (r->fif == 2) ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
+    return ARX_OK;
+}
+
 arx_status ensure_device_scene(arx_renderer* r) {
     if (!r->scene_img) return fail(ARX_ERR_NOT_READY, "arx_set_scene has not been called");
-    if (r->scene_dirty || r->recv_model_dirty || r->recv_pose_dirty || !r->qgrid_set) {
+    const bool writes = r->scene_dirty || r->recv_model_dirty || r->recv_pose_dirty || !r->qgrid_set;
+    if (writes) {
         // the uploads, re-quantization and receiver refit below write the tree the other frame in
         // flight may still be tracing
         const arx_status st = fif_wait_traced(r);
@@ -491,6 +502,10 @@ arx_status ensure_device_scene(arx_renderer* r) {
     r->scene_dirty = false;
     r->recv_model_dirty = false;
     r->recv_pose_dirty = false;
+    if (writes) {  // the other frame set's next trace waits for these writes
+        const arx_status st = fif_done(r, r->ev_scene);
+        if (st != ARX_OK) return st;
+    }
     r->stats.n_scene_tris = img.n_input;
     r->stats.n_receiver_tris = (int64_t)r->recv.tris.size();
     r->stats.n_nodes = (int64_t)n_nodes;
@@ -892,15 +907,6 @@ void free_frame_set(arx_renderer::FrameSet& f) {
     if (f.h_counters) hipHostFree(f.h_counters);
     f = arx_renderer::FrameSet{};
 }
-// wait: the current frame set's stream on the other set's event (frames in flight only)
-arx_status fif_wait(arx_renderer* r, hipEvent_t (&ev)[2]) {
-    if (r->fif == 2) ARX_HIP(hipStreamWaitEvent(r->stream, ev[r->slot ^ 1], 0));
-    return ARX_OK;
-}
-arx_status fif_done(arx_renderer* r, hipEvent_t (&ev)[2]) {
-    if (r->fif == 2) ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
-    return ARX_OK;
-}
 }  // namespace
 
 arx_status arx::fif_wait_traced(arx_renderer* r) { return fif_wait(r, r->ev_traced); }
@@ -983,7 +989,7 @@ void arx_destroy(arx_renderer* r) {
     if (r->alt.stream) hipStreamSynchronize(r->alt.stream);
     free_frame_set(r->alt);
     for (int k = 0; k < 2; ++k)
-        for (hipEvent_t e : {r->ev_traced[k], r->ev_conv[k], r->ev_reduced[k]})
+        for (hipEvent_t e : {r->ev_traced[k], r->ev_conv[k], r->ev_reduced[k], r->ev_scene[k]})
             if (e) hipEventDestroy(e);
     for (arx_stream* s : r->streams) release_stream(s);  // the handles stay valid but detached
     r->streams.clear();
@@ -1214,6 +1220,9 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         a.prof = r->d_prof;
     }
 #endif
+    // frames in flight: after the other frame set's last writes to the tree (its refit, re-gridding
+    // or upload), which this launch reads
+    if (const arx_status w = fif_wait(r, r->ev_scene); w != ARX_OK) return w;
     const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
     const int fmt = a.wbuf ? kFmtW4 : (a.qnodes ? kFmtQ16 : kFmtF32);
     // the instance launch_trace takes (ray pool or small launch): the profile guard reads these
@@ -1269,7 +1278,7 @@ arx_status arx_set_frames_in_flight(arx_renderer* r, int32_t n) {
         return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own streams (arx_set_stream)");
     if (r->d_hist_ext) return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own histograms");
     for (int k = 0; k < 2; ++k)
-        for (hipEvent_t* e : {&r->ev_traced[k], &r->ev_conv[k], &r->ev_reduced[k]})
+        for (hipEvent_t* e : {&r->ev_traced[k], &r->ev_conv[k], &r->ev_reduced[k], &r->ev_scene[k]})
             if (!*e) ARX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     arx_renderer::FrameSet f;
     const size_t bins = 2 * (size_t)r->ir_len;

@@ -190,7 +190,8 @@ struct arx_renderer {
     // Frame k + 1 waits only where the two meet: writes to the shared scene / receiver buffers wait
     // for the other set's last trace (ev_traced), uses of the shared convolution plans (and of the
     // caller's output buffers) for its last convolution (ev_conv), a group's all-reduce for its last
-    // all-reduce on the same communicator (ev_reduced).  `slot` names the set in the fields above.
+    // all-reduce on the same communicator (ev_reduced), and every trace for the other set's last
+    // scene writes (ev_scene).  `slot` names the set in the fields above.
     struct FrameSet {
         hipStream_t stream = nullptr;
         unsigned long long* d_hist = nullptr;
@@ -204,6 +205,7 @@ struct arx_renderer {
     int32_t slot = 0;
     FrameSet alt;
     hipEvent_t ev_traced[2] = {}, ev_conv[2] = {}, ev_reduced[2] = {};
+    hipEvent_t ev_scene[2] = {};  // the set's last writes to the shared scene buffers: the other set's traces wait for them
 
     unsigned long long* d_prof = nullptr;  // per-wave records (profiling builds, ARX_TRACE_PROF)
     size_t prof_words = 0;
