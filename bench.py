@@ -434,9 +434,11 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
-    ap.add_argument("--frames-in-flight", type=int, choices=(1, 2), default=2,
+    ap.add_argument("--frames-in-flight", type=int, choices=(1, 2), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
-                         "with 2, step k+1's trace starts while step k finishes; a single-frame leg is timed too")
+                         "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
+                         "too.  Default 2 on one GPU, 1 for N > 1 (the two-stream all-reduce order on one "
+                         "communicator has not run on a multi-GPU node yet)")
     ap.add_argument("--pipelined", action="store_true", help="also time two renderer groups alternating frames")
     ap.add_argument("--no-pipelined", action="store_true", help="(default; kept for older scripts)")
     ap.add_argument("--process-group", action="store_true",
@@ -509,6 +511,8 @@ def main(argv=None) -> int:
         for m, (x, ol, orr) in zip(members, bufs):
             m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
+    if args.frames_in_flight is None:
+        args.frames_in_flight = 2 if world == 1 else 1
     g.set_frames_in_flight(args.frames_in_flight)
     # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
     # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
