@@ -115,7 +115,7 @@ def test_oversubscribed_group_two_frames_in_flight(conference):
             g.set_frames_in_flight(fif)
             g.setEmitterPosInOptix(CONFERENCE_EMITTER)
             out = []
-            for lst, yaw, _, seed in FRAMES[:3]:
+            for lst, yaw, _, seed in FRAMES[1:4]:  # moved, off the grid, back in the room
                 g.setSphereCenterInOptix(lst, yaw)
                 g.set_seed(seed)
                 g.render(timed=False)
@@ -123,6 +123,7 @@ def test_oversubscribed_group_two_frames_in_flight(conference):
             irs[fif] = out
         finally:
             g.close()
+    assert irs[1][0][0].any()
     assert np.array_equal(bits(irs[1][0][0]), bits(irs[2][0][0])) and np.array_equal(bits(irs[1][0][1]), bits(irs[2][0][1]))
 
 
