@@ -47,15 +47,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
     # configs[2]: conference, 1M rays x 16 bounces, 48 kHz IR + convolution (per GPU)
-    "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, audio="clapper",
+    # fif: frames in flight on one GPU (2: a frame's tail overlaps the next frame's start; the 48 ms
+    # C4 launch loses 5 % that way, profiles/r04/bench_c4_r04m.json)
+    "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, audio="clapper", fif=2,
                desc="configs[2]: conference stand-in, 1M rays x 16 bounces per GPU, 48 kHz IR (96000 bins/ear), "
                     "file-mode FFT convolution of A_Clapper_Board.wav ch0 (807498 frames) per GPU"),
     # configs[1]: conference, 100K rays x 8 bounces, 16 kHz
-    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento",
+    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento", fif=2,
                desc="configs[1]: conference stand-in, 100K rays x 8 bounces per GPU, 16 kHz IR, "
                     "convolution of experimento_entrada_16KHz.wav (128000 frames) per GPU"),
     # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the GPUs (strong)
-    "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, audio="clapper", total=True,
+    "c4": dict(rays=(1000, 100, 100), max_bounces=32, sample_rate=48000, audio="clapper", total=True, fif=1,
                desc="configs[3]: conference stand-in, 10M rays x 32 bounces in total, ray-sharded across the "
                     "GPUs, 48 kHz IR, RCCL IR all-reduce; convolution of A_Clapper_Board.wav ch0 per GPU"),
 }
@@ -437,8 +439,9 @@ def main(argv=None) -> int:
     ap.add_argument("--frames-in-flight", type=int, choices=(1, 2), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
-                         "too.  Default 2 on one GPU, 1 for N > 1 (the two-stream all-reduce order on one "
-                         "communicator has not run on a multi-GPU node yet)")
+                         "too.  Default on one GPU: 2 for c2 / c3, 1 for c4 (its 48 ms launches lose 5 %% to "
+                         "the overlap); 1 for N > 1 (the two-stream all-reduce order on one communicator has "
+                         "not run on a multi-GPU node yet)")
     ap.add_argument("--pipelined", action="store_true", help="also time two renderer groups alternating frames")
     ap.add_argument("--no-pipelined", action="store_true", help="(default; kept for older scripts)")
     ap.add_argument("--process-group", action="store_true",
@@ -512,7 +515,7 @@ def main(argv=None) -> int:
             m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
     if args.frames_in_flight is None:
-        args.frames_in_flight = 2 if world == 1 else 1
+        args.frames_in_flight = wl["fif"] if world == 1 else 1
     g.set_frames_in_flight(args.frames_in_flight)
     # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
     # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
