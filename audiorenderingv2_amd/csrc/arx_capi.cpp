@@ -1208,6 +1208,8 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         }
         a.gstack = r->d_gstack;
         a.gstack_lanes = lanes;
+        // one global stack per renderer: with two frames in flight, after the other frame's trace
+        if (const arx_status w = fif_wait(r, r->ev_traced); w != ARX_OK) return w;
     }
 #if ARX_TRACE_PROF  // measurement builds only: per-wave records (arx_debug_trace_profile)
     {
