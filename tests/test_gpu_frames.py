@@ -71,11 +71,13 @@ def audio():
     return (0.5 * np.sin(2 * np.pi * 440 * np.arange(3 * 16000 + 321) / 16000)).astype(np.float32)
 
 
-def test_renderer_two_frames_in_flight_equal_one_at_a_time(conference, audio):
+@pytest.mark.parametrize("trace_path", [0, 2, 8])  # 16-bit BVH2 + LDS stack; global stack; CW4
+def test_renderer_two_frames_in_flight_equal_one_at_a_time(conference, audio, trace_path):
     res = {}
     for fif in (1, 2):
         r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
         try:
+            r.set_trace_path(trace_path)
             res[fif] = run_sequence(r, [r], audio, fif)
         finally:
             r.close()
