@@ -250,13 +250,29 @@ arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris) {
     return ARX_OK;
 }
 
-// wait: the current frame set's stream on the other set's event (frames in flight only)
-arx_status fif_wait(arx_renderer* r, hipEvent_t (&ev)[2]) {
-    if (r->fif == 2) ARX_HIP(hipStreamWaitEvent(r->stream, ev[r->slot ^ 1], 0));
+// Frames in flight (no-ops with one): the current set's stream waits for every other set's last
+// trace / for the set that did the last step of a chain (convolutions, all-reduces, scene writes),
+// and records its own.
+using FifEvents = hipEvent_t[arx_renderer::kMaxFrames];
+arx_status fif_wait_all(arx_renderer* r, FifEvents& ev) {
+    if (r->fif > 1)
+        for (int s = 0; s < r->fif; ++s)
+            if (s != r->slot) ARX_HIP(hipStreamWaitEvent(r->stream, ev[s], 0));
     return ARX_OK;
 }
-arx_status fif_done(arx_renderer* r, hipEvent_t (&ev)[2]) {
-    if (r->fif == 2) ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
+arx_status fif_done_one(arx_renderer* r, FifEvents& ev) {
+    if (r->fif > 1) ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
+    return ARX_OK;
+}
+arx_status fif_wait_last(arx_renderer* r, FifEvents& ev, int32_t last) {
+    if (r->fif > 1 && last >= 0 && last != r->slot) ARX_HIP(hipStreamWaitEvent(r->stream, ev[last], 0));
+    return ARX_OK;
+}
+arx_status fif_done_last(arx_renderer* r, FifEvents& ev, int32_t& last) {
+    if (r->fif > 1) {
+        ARX_HIP(hipEventRecord(ev[r->slot], r->stream));
+        last = r->slot;
+    }
     return ARX_OK;
 }
 
@@ -503,7 +519,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
     r->recv_model_dirty = false;
     r->recv_pose_dirty = false;
     if (writes) {  // the other frame set's next trace waits for these writes
-        const arx_status st = fif_done(r, r->ev_scene);
+        const arx_status st = fif_done_last(r, r->ev_scene, r->last_scene);
         if (st != ARX_OK) return st;
     }
     r->stats.n_scene_tris = img.n_input;
@@ -909,16 +925,20 @@ void free_frame_set(arx_renderer::FrameSet& f) {
 }
 }  // namespace
 
-arx_status arx::fif_wait_traced(arx_renderer* r) { return fif_wait(r, r->ev_traced); }
-arx_status arx::fif_wait_conv(arx_renderer* r) { return fif_wait(r, r->ev_conv); }
-arx_status arx::fif_wait_reduced(arx_renderer* r) { return fif_wait(r, r->ev_reduced); }
-arx_status arx::fif_done_reduced(arx_renderer* r) { return fif_done(r, r->ev_reduced); }
+arx_status arx::fif_wait_traced(arx_renderer* r) { return fif_wait_all(r, r->ev_traced); }
+arx_status arx::fif_wait_conv(arx_renderer* r) { return fif_wait_last(r, r->ev_conv, r->last_conv); }
+arx_status arx::fif_wait_reduced(arx_renderer* r) { return fif_wait_last(r, r->ev_reduced, r->last_reduced); }
+arx_status arx::fif_done_reduced(arx_renderer* r) { return fif_done_last(r, r->ev_reduced, r->last_reduced); }
 arx_status arx::sync_renderer(arx_renderer* r) {
     ARX_HIP(hipSetDevice(r->cfg.device));
     if (r->stream) ARX_HIP(hipStreamSynchronize(r->stream));
-    if (r->alt.stream) ARX_HIP(hipStreamSynchronize(r->alt.stream));
+    for (const auto& f : r->alt)
+        if (f.stream) ARX_HIP(hipStreamSynchronize(f.stream));
     return ARX_OK;
 }
+namespace {
+arx_status fif_done_conv(arx_renderer* r) { return fif_done_last(r, r->ev_conv, r->last_conv); }
+}  // namespace
 
 extern "C" {
 
@@ -986,9 +1006,11 @@ void arx_destroy(arx_renderer* r) {
     if (!r) return;
     hipSetDevice(r->cfg.device);
     if (r->stream) hipStreamSynchronize(r->stream);
-    if (r->alt.stream) hipStreamSynchronize(r->alt.stream);
-    free_frame_set(r->alt);
-    for (int k = 0; k < 2; ++k)
+    for (auto& f : r->alt) {
+        if (f.stream) hipStreamSynchronize(f.stream);
+        free_frame_set(f);
+    }
+    for (int k = 0; k < arx_renderer::kMaxFrames; ++k)
         for (hipEvent_t e : {r->ev_traced[k], r->ev_conv[k], r->ev_reduced[k], r->ev_scene[k]})
             if (e) hipEventDestroy(e);
     for (arx_stream* s : r->streams) release_stream(s);  // the handles stay valid but detached
@@ -1122,16 +1144,20 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed) {
 arx_status arx_clear_histogram(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     ARX_HIP(hipSetDevice(r->cfg.device));
-    if (r->fif == 2) {  // a frame starts: it takes the other stream, histogram, IR, counters and directions
-        std::swap(r->own_stream, r->alt.stream);
+    if (r->fif > 1) {  // a frame starts: it takes the next set's stream, histogram, IR, counters and directions
+        arx_renderer::FrameSet cur{r->own_stream, r->d_hist, r->d_ir, r->d_counters, r->h_counters, r->d_dirs, r->dirs_cap};
+        const arx_renderer::FrameSet& nx = r->alt[0];
+        r->own_stream = nx.stream;
         r->stream = r->own_stream;
-        std::swap(r->d_hist, r->alt.d_hist);
-        std::swap(r->d_ir, r->alt.d_ir);
-        std::swap(r->d_counters, r->alt.d_counters);
-        std::swap(r->h_counters, r->alt.h_counters);
-        std::swap(r->d_dirs, r->alt.d_dirs);
-        std::swap(r->dirs_cap, r->alt.dirs_cap);
-        r->slot ^= 1;
+        r->d_hist = nx.d_hist;
+        r->d_ir = nx.d_ir;
+        r->d_counters = nx.d_counters;
+        r->h_counters = nx.h_counters;
+        r->d_dirs = nx.d_dirs;
+        r->dirs_cap = nx.dirs_cap;
+        for (int i = 0; i + 1 < r->fif - 1; ++i) r->alt[i] = r->alt[i + 1];
+        r->alt[r->fif - 2] = cur;
+        r->slot = (r->slot + 1) % r->fif;
     }
     ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
     return ARX_OK;
@@ -1208,8 +1234,8 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
         }
         a.gstack = r->d_gstack;
         a.gstack_lanes = lanes;
-        // one global stack per renderer: with two frames in flight, after the other frame's trace
-        if (const arx_status w = fif_wait(r, r->ev_traced); w != ARX_OK) return w;
+        // one global stack per renderer: with frames in flight, after the other frames' traces
+        if (const arx_status w = fif_wait_all(r, r->ev_traced); w != ARX_OK) return w;
     }
 #if ARX_TRACE_PROF  // measurement builds only: per-wave records (arx_debug_trace_profile)
     {
@@ -1224,7 +1250,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
 #endif
     // frames in flight: after the other frame set's last writes to the tree (its refit, re-gridding
     // or upload), which this launch reads
-    if (const arx_status w = fif_wait(r, r->ev_scene); w != ARX_OK) return w;
+    if (const arx_status w = fif_wait_last(r, r->ev_scene, r->last_scene); w != ARX_OK) return w;
     const int slot = (int)(r->trace_launches % arx_renderer::kTraceRing);
     const int fmt = a.wbuf ? kFmtW4 : (a.qnodes ? kFmtQ16 : kFmtF32);
     // the instance launch_trace takes (ray pool or small launch): the profile guard reads these
@@ -1237,7 +1263,7 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
     ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
     ++r->trace_launches;
-    return fif_done(r, r->ev_traced);
+    return fif_done_one(r, r->ev_traced);
 }
 
 arx_status arx_finalize_ir(arx_renderer* r) {
@@ -1266,39 +1292,45 @@ arx_status arx_render(arx_renderer* r, double* render_ms) {
 
 arx_status arx_set_frames_in_flight(arx_renderer* r, int32_t n) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
-    if (n != 1 && n != 2) return fail(ARX_ERR_INVALID_ARGUMENT, "frames in flight: 1 or 2, not %d", n);
+    if (n < 1 || n > arx_renderer::kMaxFrames)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "frames in flight: 1 to %d, not %d", arx_renderer::kMaxFrames, n);
     if (n == r->fif) return ARX_OK;
     ARX_HIP(hipSetDevice(r->cfg.device));
-    if (n == 1) {  // the current set stays, the other goes
-        const arx_status st = sync_renderer(r);
-        if (st != ARX_OK) return st;
-        free_frame_set(r->alt);
-        r->fif = 1;
-        return ARX_OK;
-    }
-    if (r->stream != r->own_stream)
-        return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own streams (arx_set_stream)");
-    if (r->d_hist_ext) return fail(ARX_ERR_INVALID_ARGUMENT, "two frames in flight need the renderer's own histograms");
-    for (int k = 0; k < 2; ++k)
+    if (n > 1 && r->stream != r->own_stream)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "frames in flight need the renderer's own streams (arx_set_stream)");
+    if (n > 1 && r->d_hist_ext) return fail(ARX_ERR_INVALID_ARGUMENT, "frames in flight need the renderer's own histograms");
+    // nothing of the old arrangement stays in flight: the sets' order and the event slots start over
+    const arx_status st = sync_renderer(r);
+    if (st != ARX_OK) return st;
+    for (int k = n - 1; k < arx_renderer::kMaxFrames - 1; ++k) free_frame_set(r->alt[k]);  // the current set stays
+    for (int k = 0; k < n; ++k)
         for (hipEvent_t* e : {&r->ev_traced[k], &r->ev_conv[k], &r->ev_reduced[k], &r->ev_scene[k]})
             if (!*e) ARX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    arx_renderer::FrameSet f;
     const size_t bins = 2 * (size_t)r->ir_len;
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipMalloc(&f.d_hist, bins * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipMalloc(&f.d_ir, bins * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&f.d_counters, (kCursor + 1) * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipHostMalloc(&f.h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipMemsetAsync(f.d_hist, 0, bins * sizeof(unsigned long long), f.stream)) != hipSuccess ||
-        (e = hipMemsetAsync(f.d_ir, 0, bins * sizeof(float), f.stream)) != hipSuccess ||
-        (e = hipMemsetAsync(f.d_counters, 0, (kCursor + 1) * sizeof(unsigned long long), f.stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(f.stream)) != hipSuccess) {
-        free_frame_set(f);
-        return fail(ARX_ERR_HIP, "arx_set_frames_in_flight: %s", hipGetErrorString(e));
+    for (int k = 0; k < n - 1; ++k) {
+        if (r->alt[k].stream) continue;
+        arx_renderer::FrameSet f;
+        hipError_t e;
+        if ((e = hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipMalloc(&f.d_hist, bins * sizeof(unsigned long long))) != hipSuccess ||
+            (e = hipMalloc(&f.d_ir, bins * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&f.d_counters, (kCursor + 1) * sizeof(unsigned long long))) != hipSuccess ||
+            (e = hipHostMalloc(&f.h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+            (e = hipMemsetAsync(f.d_hist, 0, bins * sizeof(unsigned long long), f.stream)) != hipSuccess ||
+            (e = hipMemsetAsync(f.d_ir, 0, bins * sizeof(float), f.stream)) != hipSuccess ||
+            (e = hipMemsetAsync(f.d_counters, 0, (kCursor + 1) * sizeof(unsigned long long), f.stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(f.stream)) != hipSuccess) {
+            free_frame_set(f);
+            for (int q = 0; q < arx_renderer::kMaxFrames - 1; ++q) free_frame_set(r->alt[q]);
+            r->fif = 1;
+            r->slot = 0;
+            return fail(ARX_ERR_HIP, "arx_set_frames_in_flight: %s", hipGetErrorString(e));
+        }
+        r->alt[k] = f;
     }
-    r->alt = f;
-    r->fif = 2;
+    r->fif = n;
+    r->slot = 0;
+    r->last_conv = r->last_reduced = r->last_scene = -1;
     return ARX_OK;
 }
 
@@ -1432,7 +1464,7 @@ arx_status arx_prepare_ir_spectra(arx_renderer* r, int which) {
     arx_status st = fif_wait_conv(r);
     if (st == ARX_OK && (which & 1)) st = ensure_conv(r);
     if (st == ARX_OK && (which & 2)) st = ensure_conv_live(r, 1);
-    return st == ARX_OK ? fif_done(r, r->ev_conv) : st;
+    return st == ARX_OK ? fif_done_conv(r) : st;
 }
 
 arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len) {
@@ -1443,7 +1475,7 @@ arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len) 
     if (st == ARX_OK) st = which == 1 ? ensure_conv(r) : ensure_conv_live(r, 1);
     if (st != ARX_OK) return st;
     std::snprintf(buf, len, "%s", conv_plan_describe(which == 1 ? r->conv : r->conv_live));
-    return fif_done(r, r->ev_conv);
+    return fif_done_conv(r);
 }
 
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
@@ -1463,7 +1495,7 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     r->conv_ir_dirty = false;
     ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
     ++r->conv_launches;
-    return fif_done(r, r->ev_conv);
+    return fif_done_conv(r);
 }
 
 arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t in_bytes, float* h_out_left,
@@ -1524,7 +1556,7 @@ arx_status arx_convolute_live_device(arx_renderer* r, const double* d_in, size_t
     ARX_HIP(conv_run_live(r->conv_live, d_in, (int64_t)n_in, d_out, r->stream));
     ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
     ++r->live_launches;
-    return fif_done(r, r->ev_conv);
+    return fif_done_conv(r);
 }
 
 arx_status arx_convolute_live_block(arx_renderer* r, const double* h_in, size_t in_bytes, double* h_out,
@@ -1652,7 +1684,7 @@ arx_status arx_stream_reset(arx_stream* s) {
     ARX_HIP(hipSetDevice(s->r->cfg.device));
     if (const arx_status w = fif_wait_conv(s->r); w != ARX_OK) return w;
     ARX_HIP(stream_reset(s->plan, s->r->stream));
-    return fif_done(s->r, s->r->ev_conv);
+    return fif_done_conv(s->r);
 }
 
 arx_status arx_stream_info(const arx_stream* s, int32_t* block, int32_t* partitions, int32_t* fft_size) {
@@ -1681,7 +1713,7 @@ arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n
     ARX_HIP(stream_run(s->plan, d_in, (int64_t)n_frames, d_out, r->stream));
     ARX_HIP(hipEventRecord(r->lev1[slot], r->stream));
     ++r->live_launches;
-    return fif_done(r, r->ev_conv);
+    return fif_done_conv(r);
 }
 
 arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames, double* h_out, size_t out_len) {

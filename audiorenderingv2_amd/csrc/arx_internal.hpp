@@ -184,14 +184,16 @@ struct arx_renderer {
 
     std::vector<arx_stream*> streams;  // live streaming convolutions of this renderer (arx_stream_create)
 
-    // Frames in flight (arx_set_frames_in_flight): with 2, a frame's start (arx_clear_histogram)
-    // swaps the stream, histogram, IR, counters and direction buffer above with this second set, so
-    // frame k + 1 traces on its own stream while frame k's trace finishes and its IR is convolved.
-    // Frame k + 1 waits only where the two meet: writes to the shared scene / receiver buffers wait
-    // for the other set's last trace (ev_traced), uses of the shared convolution plans (and of the
-    // caller's output buffers) for its last convolution (ev_conv), a group's all-reduce for its last
-    // all-reduce on the same communicator (ev_reduced), and every trace for the other set's last
-    // scene writes (ev_scene).  `slot` names the set in the fields above.
+    // Frames in flight (arx_set_frames_in_flight, up to kMaxFrames): a frame's start
+    // (arx_clear_histogram) rotates the stream, histogram, IR, counters and direction buffer above
+    // with the sets in `alt`, so frame k + 1 traces on its own stream while frame k's trace finishes
+    // and its IR is convolved.  The frames wait for each other only where they share state: writes to
+    // the shared scene / receiver buffers (and traces on the one global stack) for every other set's
+    // last trace (ev_traced); each trace for the last scene writes (ev_scene), each use of the shared
+    // convolution plans and of the caller's output buffers for the last convolution (ev_conv), a
+    // group's all-reduce for the last all-reduce on the same communicator (ev_reduced).  `slot` names
+    // the set in the fields above; last_* the set that did the last such step (-1: none yet).
+    static constexpr int kMaxFrames = 3;
     struct FrameSet {
         hipStream_t stream = nullptr;
         unsigned long long* d_hist = nullptr;
@@ -203,9 +205,10 @@ struct arx_renderer {
     };
     int32_t fif = 1;
     int32_t slot = 0;
-    FrameSet alt;
-    hipEvent_t ev_traced[2] = {}, ev_conv[2] = {}, ev_reduced[2] = {};
-    hipEvent_t ev_scene[2] = {};  // the set's last writes to the shared scene buffers: the other set's traces wait for them
+    FrameSet alt[kMaxFrames - 1];
+    hipEvent_t ev_traced[kMaxFrames] = {}, ev_conv[kMaxFrames] = {}, ev_reduced[kMaxFrames] = {},
+               ev_scene[kMaxFrames] = {};
+    int32_t last_conv = -1, last_reduced = -1, last_scene = -1;
 
     unsigned long long* d_prof = nullptr;  // per-wave records (profiling builds, ARX_TRACE_PROF)
     size_t prof_words = 0;

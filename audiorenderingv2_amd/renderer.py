@@ -145,8 +145,8 @@ class AudioRenderer:
         kept so callers of that API keep working (the live path zips L/R on the device)."""
 
     def set_frames_in_flight(self, n: int) -> None:
-        """1 or 2 (arx_set_frames_in_flight): with 2, consecutive render() calls alternate between
-        two streams and buffers, so a render / convolute loop keeps the GPU full; every getter and
+        """1 to 3 (arx_set_frames_in_flight): with n > 1, consecutive render() calls rotate over n
+        streams and buffer sets, so a render / convolute loop keeps the GPU full; every getter and
         convolution refers to the last frame started."""
         check(lib().arx_set_frames_in_flight(self._h, int(n)))
 

@@ -47,13 +47,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
     # configs[2]: conference, 1M rays x 16 bounces, 48 kHz IR + convolution (per GPU)
-    # fif: frames in flight on one GPU (2: a frame's tail overlaps the next frame's start; the 48 ms
-    # C4 launch loses 5 % that way, profiles/r04/bench_c4_r04m.json)
+    # fif: frames in flight on one GPU (a frame's tail overlaps the next frames' start): C3 +3 % with 2,
+    # no more with 3; C2, whose single frame fills 1.5 waves per SIMD, +62 % with 2 and +112 % with 3;
+    # the 48 ms C4 launch loses 5 % with 2 (profiles/r04/bench_*_fif*_r04p.json, bench_c4_r04m.json)
     "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, audio="clapper", fif=2,
                desc="configs[2]: conference stand-in, 1M rays x 16 bounces per GPU, 48 kHz IR (96000 bins/ear), "
                     "file-mode FFT convolution of A_Clapper_Board.wav ch0 (807498 frames) per GPU"),
     # configs[1]: conference, 100K rays x 8 bounces, 16 kHz
-    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento", fif=2,
+    "c2": dict(rays=(100, 100, 10), max_bounces=8, sample_rate=16000, audio="experimento", fif=3,
                desc="configs[1]: conference stand-in, 100K rays x 8 bounces per GPU, 16 kHz IR, "
                     "convolution of experimento_entrada_16KHz.wav (128000 frames) per GPU"),
     # configs[3]: conference, 10M rays x 32 bounces in total, ray-sharded over the GPUs (strong)
@@ -436,11 +437,11 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
-    ap.add_argument("--frames-in-flight", type=int, choices=(1, 2), default=None,
+    ap.add_argument("--frames-in-flight", type=int, choices=(1, 2, 3), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
-                         "too.  Default on one GPU: 2 for c2 / c3, 1 for c4 (its 48 ms launches lose 5 %% to "
-                         "the overlap); 1 for N > 1 (the two-stream all-reduce order on one communicator has "
+                         "too.  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 48 ms launches lose 5 %% "
+                         "to the overlap); 1 for N > 1 (the two-stream all-reduce order on one communicator has "
                          "not run on a multi-GPU node yet)")
     ap.add_argument("--pipelined", action="store_true", help="also time two renderer groups alternating frames")
     ap.add_argument("--no-pipelined", action="store_true", help="(default; kept for older scripts)")

@@ -147,8 +147,8 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed);
  * N rays, finalize the stereo IR (mono merge = addIRs, kernels.cu:519-527).  render_ms gets the
  * trace kernel's device time (the reference's timed window, :495-518). */
 arx_status arx_render(arx_renderer* r, double* render_ms);
-/* Frames in flight (n = 1 or 2; no reference equivalent -- its render() blocks, AudioRenderer.cpp:
- * 489-523).  With 2, consecutive render() calls alternate between two streams, histograms and IRs:
+/* Frames in flight (n = 1 to 3; no reference equivalent -- its render() blocks, AudioRenderer.cpp:
+ * 489-523).  With n > 1, consecutive render() calls rotate over n streams, histograms and IRs:
  * frame k + 1 traces while frame k's trace finishes and its IR is convolved, so a render/convolute
  * loop keeps the GPU full.  Results are those of one frame at a time, bit for bit: every getter,
  * convolution and IR copy refers to the last frame started, and the two frames meet only where they

@@ -71,17 +71,18 @@ def audio():
     return (0.5 * np.sin(2 * np.pi * 440 * np.arange(3 * 16000 + 321) / 16000)).astype(np.float32)
 
 
-@pytest.mark.parametrize("trace_path", [0, 2, 8])  # 16-bit BVH2 + LDS stack; global stack; CW4
-def test_renderer_two_frames_in_flight_equal_one_at_a_time(conference, audio, trace_path):
+# 16-bit BVH2 + LDS stack, global stack, CW4 with two frames in flight; three frames
+@pytest.mark.parametrize("trace_path,frames", [(0, 2), (2, 2), (8, 2), (0, 3)])
+def test_renderer_frames_in_flight_equal_one_at_a_time(conference, audio, trace_path, frames):
     res = {}
-    for fif in (1, 2):
+    for fif in (1, frames):
         r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
         try:
             r.set_trace_path(trace_path)
             res[fif] = run_sequence(r, [r], audio, fif)
         finally:
             r.close()
-    (o1, s1, ir1, st1), (o2, s2, ir2, st2) = res[1], res[2]
+    (o1, s1, ir1, st1), (o2, s2, ir2, st2) = res[1], res[frames]
     assert ir1[0].any() and st1[1] > 0
     for k, (a, b) in enumerate(zip(o1, o2)):
         assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1])), f"frame {k}"
@@ -133,7 +134,7 @@ def test_frames_in_flight_refuses_a_callers_stream_or_histogram():
     r = AudioRenderer(RenderSettings(rays=(4, 4, 4), sample_rate=16000))
     try:
         with pytest.raises(ArxError):
-            r.set_frames_in_flight(3)
+            r.set_frames_in_flight(4)
         r.set_frames_in_flight(2)
         with pytest.raises(ArxError):
             r.set_stream(r.get_stream())
