@@ -313,41 +313,6 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
                          "(projected 8-GPU rank) + the modelled all-reduce"}
 
 
-def pipelined_leg(groups, bufs, frames: int, steps: int, warmup: int, ranks: "Ranks", one_frame_ms: float) -> dict:
-    """Two frames in flight: a second renderer group on the same GPUs (same settings; the scene
-    tree is libarx's cached build, not a second one), each group on its own HIP streams, steps
-    alternating between them.  Step k's trace can then fill the SIMDs step k-1's persistent waves
-    leave as they finish (the launch tail), and a latency-bound launch (C2: about one ray per lane)
-    shares the GPU with the next one.  Same per-step work and results as the headline loop (the
-    IRs are compared); reported beside it, not as `value`."""
-    def step(k):
-        g = groups[k % len(groups)]
-        g.render(timed=False)
-        for m, (x, ol, orr) in zip(g.members, bufs[k % len(groups)]):
-            m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
-
-    for k in range(warmup * len(groups)):
-        step(k)
-    for g in groups:
-        g.synchronize()
-    ranks.barrier()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        step(k)
-    for g in groups:
-        g.synchronize()
-    ranks.barrier()
-    elapsed = ranks.max(time.perf_counter() - t0)
-    q = int(round(ranks.sum(sum(int(g.stats()["queries"]) for g in groups) / len(groups))))
-    a, b = groups[0].member(0).get_ir(), groups[1].member(0).get_ir()
-    same = bool(np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32)) and
-                np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)))
-    ms = elapsed / steps * 1e3
-    return {"frames_in_flight": len(groups), "value": q * steps / elapsed, "unit": "ray-bounces/s", "steps": steps,
-            "ms_per_step": ms, "speedup_vs_one_frame": one_frame_ms / ms, "irs_identical": same,
-            "method": "two renderer groups (shared scene build), own streams, steps alternating; wall clock of K steps"}
-
-
 def streaming_leg(m, audio, block: int) -> dict:
     """C3's streaming overlap-add leg: the same audio fed through the streaming convolution
     (arx_stream_*: uniformly partitioned overlap-save, f64) in 4096-frame blocks, device-resident
@@ -443,8 +408,8 @@ def main(argv=None) -> int:
                          "too.  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 48 ms launches lose 5 %% "
                          "to the overlap); 1 for N > 1 (the two-stream all-reduce order on one communicator has "
                          "not run on a multi-GPU node yet)")
-    ap.add_argument("--pipelined", action="store_true", help="also time two renderer groups alternating frames")
-    ap.add_argument("--no-pipelined", action="store_true", help="(default; kept for older scripts)")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
     ap.add_argument("--process-group", action="store_true",
                     help="take the one-GPU-per-process (RCCL rank) path even at one rank: a rehearsal of the "
                          "torch.distributed.run path on a one-GPU box")
@@ -584,24 +549,6 @@ def main(argv=None) -> int:
     conv_ms_max = ranks.max(max(conv_ms_all))
 
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
-    # frames in flight: a second group beside g
-    pipelined = None
-    if args.pipelined:
-        with _stdout_to_stderr():
-            if plan["mode"] == "rank":
-                g2 = RenderGroup.rank(settings, world, rank, uids[1], scene=scene, receiver=receiver)
-            else:
-                g2 = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
-        g2.setEmitterPosInOptix(CONFERENCE_EMITTER)
-        g2.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
-        bufs2 = [(DeviceBuffer.from_numpy(m.settings.device, audio_np), DeviceBuffer(m.settings.device, 4 * frames),
-                  DeviceBuffer(m.settings.device, 4 * frames)) for m in g2.members]
-        pipelined = pipelined_leg([g, g2], [bufs, bufs2], frames, args.steps, args.warmup, ranks,
-                                  elapsed / args.steps * 1e3)
-        for b in bufs2:
-            for x in b:
-                x.close()
-        g2.close()
     moving = None
     if args.c5_frames > 0:  # C5 on a group of its own: 1M rays per frame in total, sharded over the GPUs
         s5 = RenderSettings(rays=C5["rays"], ir_length_in_seconds=2, sample_rate=C5["sample_rate"], base_power=3.62,
@@ -752,8 +699,6 @@ def main(argv=None) -> int:
                                 device=plan["devices"][0])
             result["moving_listener_rank_of_8"] = moving_listener_rank_shape(s5, scene, receiver, args.c5_frames,
                                                                              int(np.prod(C5["rays"])) // 8)
-    if pipelined is not None:
-        result["pipelined"] = pipelined
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
         result["streaming"] = streaming_leg(m0, audio_np, 4096)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
