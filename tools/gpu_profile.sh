@@ -2,6 +2,8 @@
 # PMC traffic (FETCH_SIZE / WRITE_SIZE, separate passes), pipeline state counters, the counting
 # build's lane loads per query, and the guarded profile JSONs bench.py reads (tree hash + VGPRs).
 # Outputs under gpurun_out/$RD/ (default r04).  TAG names the files.
+# Build the counting library here first (it is not kept in the tree between rounds):
+#   python -m audiorenderingv2_amd.build --exp count -D ARX_TRACE_COUNT=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
