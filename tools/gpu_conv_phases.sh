@@ -1,7 +1,7 @@
 # Per-workgroup phases of the C3 convolution (tools/conv_phases.py, measurement build libarx_cprof.so)
 # and the standalone per-pass kernel times (rocprofv3) of the product library; outputs under
-# Build it here first: python -m audiorenderingv2_amd.build --exp cprof -D ARX_CONV_PROF=1
 # gpurun_out/$RD/.
+# Build it here first: python -m audiorenderingv2_amd.build --exp cprof -D ARX_CONV_PROF=1
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
