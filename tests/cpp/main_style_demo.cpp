@@ -92,7 +92,8 @@ static void write_raw(const std::string& path, const void* data, size_t bytes) {
 
 int main(int argc, char** argv) {
     if (argc < 6) {
-        std::fprintf(stderr, "usage: main_style_demo config.json leftHalf.obj rightHalf.obj out_dir angle_deg\n");
+        std::fprintf(stderr,
+                     "usage: main_style_demo config.json leftHalf.obj rightHalf.obj out_dir angle_deg [frames_in_flight]\n");
         return 2;
     }
     const std::string out = argv[4];
@@ -106,6 +107,7 @@ int main(int argc, char** argv) {
         AudioRenderer* renderer = new AudioRenderer(&model, cfg.ir_length_in_seconds, wav.sample_rate,
                                                     configMaterials(cfg),
                                                     gdt::vec3f(cfg.rays[0], cfg.rays[1], cfg.rays[2]));
+        if (argc > 6) renderer->setFramesInFlight(std::atoi(argv[6]));  // not in main.cpp: the renderer mode
         renderer->setMonoOutput(cfg.mono != 0);
         renderer->setBasePower(cfg.base_power);
         renderer->setThresholds(cfg.ray_energy_threshold, cfg.ray_max_bounces);

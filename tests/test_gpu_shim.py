@@ -210,14 +210,17 @@ def test_cpp_shim_c4_sharded_equals_python_group(demo):
     assert np.array_equal(np.fromfile(out / "ir_right.f32", np.float32).view(np.uint32), gr.view(np.uint32))
 
 
-def test_main_style_full_render_matches_oracle(demo):
+@pytest.mark.parametrize("frames", [1, 2])
+def test_main_style_full_render_matches_oracle(demo, frames):
     """main.cpp:40-67's full_render, unchanged, over the shim (tests/cpp/main_style_demo.cpp): an
     OptixModel*, a Sphere of two HalfSpheres, a gdt::vec3f camera point and glm::vec3 setters.  The file
     branch (full_render_cycle under the caller's mutex) renders with the receiver placed at the camera
     and rotated by its angle, then convolves; the live branch (placeReceiver + setSphereCenterInOptix +
     render) follows a moved, turned camera.  Both IRs bit-exact vs the oracle at those poses, the
-    convolution <= 1 ULP(max)."""
+    convolution <= 1 ULP(max).  Also with two frames in flight (setFramesInFlight): the same results."""
     d, _ = demo
+    d = d / f"main_fif{frames}"
+    d.mkdir()
     exe = str(d / "main_style_demo")
     pkg = os.path.join(REPO, "audiorenderingv2_amd")
     subprocess.run([shutil.which("g++"), "-std=c++17", "-O2", "-I", os.path.join(REPO, "include"),
@@ -244,7 +247,7 @@ def test_main_style_full_render_matches_oracle(demo):
     out = d / "out_main"
     out.mkdir()
     run = subprocess.run([exe, str(d / "config2.json"), str(d / "leftHalf.obj"), str(d / "rightHalf.obj"), str(out),
-                          str(angle)], capture_output=True, text=True, timeout=120)
+                          str(angle), str(frames)], capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stderr
     scene = scene_from_meshes(meshes, mats)
     moved = (np.float32(listener[0]) + np.float32(0.5), listener[1], np.float32(listener[2]) - np.float32(0.25))
