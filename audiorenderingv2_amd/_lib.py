@@ -173,6 +173,8 @@ SIGNATURES = {
     "arx_group_synchronize": (C.c_int, [_P]),
     "arx_group_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
     "arx_group_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),
+    "arx_debug_group_force_collectives": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "arx_debug_group_collectives": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     # input formats (host only)
     "arx_model_load_obj": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p, C.POINTER(_P)]),
     "arx_model_free": (None, [_P]),

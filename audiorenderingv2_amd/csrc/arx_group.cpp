@@ -39,6 +39,16 @@ struct arx_group {
     bool device_sum = false;             // all members on one device: sum there, no RCCL
     std::vector<hipEvent_t> traced;      // per member: its shard's trace is done
     hipEvent_t summed = nullptr;         // member 0: the on-device sum is done
+    // arx_debug_group_force_collectives: every collective issued at one rank too (a one-GPU box runs
+    // the RCCL call paths, stream order and frames-in-flight event chain the multi-GPU job takes);
+    // out_of_place: the histogram all-reduce into a receive buffer pre-filled with 0xFF, then copied
+    // back, so a one-rank collective must move the data for the IR to come out right
+    bool force_collectives = false;
+    bool out_of_place = false;
+    std::vector<unsigned long long*> d_recv;  // per member: the out-of-place receive buffer (2*ir_len)
+    // collectives the group issued (arx_debug_group_collectives): [0] histogram all-reduces, [1] f64
+    // all-reduces, [2] scene broadcasts (rank path)
+    uint64_t n_coll[3] = {0, 0, 0};
 };
 
 namespace {
@@ -51,6 +61,11 @@ namespace {
     } while (0)
 
 void destroy_members(arx_group* g) {
+    for (size_t i = 0; i < g->d_recv.size(); ++i) {
+        hipSetDevice(g->members[i]->cfg.device);
+        hipFree(g->d_recv[i]);
+    }
+    g->d_recv.clear();
     for (ncclComm_t c : g->comms)
         if (c) ncclCommDestroy(c);
     g->comms.clear();
@@ -318,7 +333,7 @@ extern "C" {
 
 arx_status arx_group_set_scene(arx_group* g, const float* tri_v, const float* tri_abs, int64_t n) {
     if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
-    const bool rank_path = g->n_ranks > 1 && g->members.size() == 1 && g->comms.size() == 1;
+    const bool rank_path = (g->n_ranks > 1 || g->force_collectives) && g->members.size() == 1 && g->comms.size() == 1;
     SceneRef img;
     if (!rank_path) {
         const arx_status st = check_scene_input(tri_v, tri_abs, n);
@@ -331,6 +346,7 @@ arx_status arx_group_set_scene(arx_group* g, const float* tri_v, const float* tr
         RcclChannel ch{g->comms[0], r->stream, g->rank0 == 0};
         const arx_status st = share_scene(ch, g->rank0, tri_v, tri_abs, n, &img);
         if (st != ARX_OK) return st;
+        ++g->n_coll[2];
     }
     return for_all(g, [&](arx_renderer* m) { return set_scene_image(m, img); });
 }
@@ -389,24 +405,43 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         if (st != ARX_OK) return st;
     }
     // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:
-    //    its communicator is kept for the group's other collectives, the render skips the no-op)
-    if (!g->comms.empty() && g->n_ranks > 1) {
-        // with two frames in flight, each member's all-reduce after its previous one (the
-        // collectives on a communicator keep their order whichever stream they run on)
+    //    its communicator is kept for the group's other collectives, the render skips the no-op
+    //    unless arx_debug_group_force_collectives asks for it)
+    if (!g->comms.empty() && (g->n_ranks > 1 || g->force_collectives)) {
+        // with frames in flight, each member's all-reduce after its previous one (the collectives on
+        // a communicator keep their order whichever stream they run on)
         for (arx_renderer* r : g->members) {
             const arx_status st = fif_wait_reduced(r);
             if (st != ARX_OK) return st;
         }
+        if (g->out_of_place) {  // the receive buffers hold 0xFF until the collective writes them
+            if (g->d_recv.size() != g->members.size()) g->d_recv.assign(g->members.size(), nullptr);
+            for (size_t i = 0; i < g->members.size(); ++i) {
+                arx_renderer* r = g->members[i];
+                ARX_HIP(hipSetDevice(r->cfg.device));
+                if (!g->d_recv[i]) ARX_HIP(hipMalloc(&g->d_recv[i], bins * sizeof(long long)));
+                ARX_HIP(hipMemsetAsync(g->d_recv[i], 0xFF, bins * sizeof(long long), r->stream));
+            }
+        }
         ARX_NCCL(ncclGroupStart());
         for (size_t i = 0; i < g->members.size(); ++i) {
             arx_renderer* r = g->members[i];
-            const ncclResult_t e = ncclAllReduce(r->hist(), r->hist(), bins, ncclInt64, ncclSum, g->comms[i], r->stream);
+            void* recv = g->out_of_place ? (void*)g->d_recv[i] : (void*)r->hist();
+            const ncclResult_t e = ncclAllReduce(r->hist(), recv, bins, ncclInt64, ncclSum, g->comms[i], r->stream);
             if (e != ncclSuccess) {
                 ncclGroupEnd();
                 return fail(ARX_ERR_HIP, "ncclAllReduce failed: %s", ncclGetErrorString(e));
             }
         }
         ARX_NCCL(ncclGroupEnd());
+        ++g->n_coll[0];
+        if (g->out_of_place)  // the sum back into the histogram the finalise reads, before the next frame's
+            for (size_t i = 0; i < g->members.size(); ++i) {  // all-reduce may write the receive buffer
+                arx_renderer* r = g->members[i];
+                ARX_HIP(hipSetDevice(r->cfg.device));
+                ARX_HIP(hipMemcpyAsync(r->hist(), g->d_recv[i], bins * sizeof(long long), hipMemcpyDeviceToDevice,
+                                       r->stream));
+            }
         for (arx_renderer* r : g->members) {
             const arx_status st = fif_done_reduced(r);
             if (st != ARX_OK) return st;
@@ -466,13 +501,16 @@ arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t
 arx_status arx_group_allreduce_f64(arx_group* g, double* values, size_t n, int op) {
     if (!g || g->members.empty() || (n > 0 && !values) || (op != 0 && op != 1))
         return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
-    if (g->comms.empty() || n == 0 || (int32_t)g->members.size() == g->n_ranks) return ARX_OK;  // one process
+    if (g->comms.empty() || n == 0 || ((int32_t)g->members.size() == g->n_ranks && !g->force_collectives))
+        return ARX_OK;  // one process (unless arx_debug_group_force_collectives)
     for (arx_renderer* r : g->members) {  // nothing of a frame in flight left ahead of this collective
         const arx_status st0 = sync_renderer(r);
         if (st0 != ARX_OK) return st0;
     }
-    // this process's values enter through member 0; the other local members add the identity
-    std::vector<double*> bufs(g->members.size(), nullptr);
+    // this process's values enter through member 0; the other local members add the identity.  Out
+    // of place (arx_debug_group_force_collectives): into receive buffers pre-filled with NaN.
+    const bool oop = g->out_of_place;
+    std::vector<double*> bufs(g->members.size(), nullptr), outs(g->members.size(), nullptr);
     std::vector<double> ident(n, op == 0 ? 0.0 : -HUGE_VAL);
     arx_status st = ARX_OK;
     for (size_t i = 0; i < g->members.size() && st == ARX_OK; ++i) {
@@ -481,29 +519,55 @@ arx_status arx_group_allreduce_f64(arx_group* g, double* values, size_t n, int o
             hipMemcpyAsync(bufs[i], i == 0 ? values : ident.data(), n * sizeof(double), hipMemcpyHostToDevice,
                            r->stream) != hipSuccess)
             st = fail(ARX_ERR_HIP, "arx_group_allreduce_f64: staging failed");
+        else if (oop && (hipMalloc(&outs[i], n * sizeof(double)) != hipSuccess ||
+                         hipMemsetAsync(outs[i], 0xFF, n * sizeof(double), r->stream) != hipSuccess))
+            st = fail(ARX_ERR_HIP, "arx_group_allreduce_f64: staging failed");
+        if (!oop) outs[i] = bufs[i];
     }
     if (st == ARX_OK) {
         ncclGroupStart();
         ncclResult_t e = ncclSuccess;
         for (size_t i = 0; i < g->members.size() && e == ncclSuccess; ++i)
-            e = ncclAllReduce(bufs[i], bufs[i], n, ncclFloat64, op == 0 ? ncclSum : ncclMax, g->comms[i],
+            e = ncclAllReduce(bufs[i], outs[i], n, ncclFloat64, op == 0 ? ncclSum : ncclMax, g->comms[i],
                               g->members[i]->stream);
         const ncclResult_t e2 = ncclGroupEnd();
         if (e != ncclSuccess || e2 != ncclSuccess)
             st = fail(ARX_ERR_HIP, "ncclAllReduce(f64) failed: %s", ncclGetErrorString(e != ncclSuccess ? e : e2));
+        else
+            ++g->n_coll[1];
     }
     if (st == ARX_OK) {
         arx_renderer* r0 = g->members[0];
         if (hipSetDevice(r0->cfg.device) != hipSuccess ||
-            hipMemcpyAsync(values, bufs[0], n * sizeof(double), hipMemcpyDeviceToHost, r0->stream) != hipSuccess)
+            hipMemcpyAsync(values, outs[0], n * sizeof(double), hipMemcpyDeviceToHost, r0->stream) != hipSuccess)
             st = fail(ARX_ERR_HIP, "arx_group_allreduce_f64: download failed");
     }
     for (size_t i = 0; i < g->members.size(); ++i) {
         hipSetDevice(g->members[i]->cfg.device);
         hipStreamSynchronize(g->members[i]->stream);
         hipFree(bufs[i]);
+        if (oop) hipFree(outs[i]);
     }
     return st;
+}
+
+arx_status arx_debug_group_force_collectives(arx_group* g, int32_t on, int32_t out_of_place) {
+    if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
+    if (on && g->comms.empty())
+        return fail(ARX_ERR_INVALID_ARGUMENT, "an oversubscribed group (one GPU listed several times) has no communicator");
+    for (arx_renderer* r : g->members) {  // nothing of a frame in flight left behind the switch
+        const arx_status st = sync_renderer(r);
+        if (st != ARX_OK) return st;
+    }
+    g->force_collectives = on != 0;
+    g->out_of_place = on != 0 && out_of_place != 0;
+    return ARX_OK;
+}
+
+arx_status arx_debug_group_collectives(const arx_group* g, uint64_t* out3) {
+    if (!g || !out3) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL argument");
+    for (int k = 0; k < 3; ++k) out3[k] = g->n_coll[k];
+    return ARX_OK;
 }
 
 arx_status arx_runtime_info(char* buf, size_t len) {

@@ -500,6 +500,17 @@ class RenderGroup:
                                             {"sum": 0, "max": 1}[op]))
         return v
 
+    def debug_force_collectives(self, on: bool = True, out_of_place: bool = False) -> None:
+        """Tests only (arx_debug_group_force_collectives): every collective issued at one rank too,
+        out of place into 0xFF-filled receive buffers if asked."""
+        check(lib().arx_debug_group_force_collectives(self._g, 1 if on else 0, 1 if out_of_place else 0))
+
+    def debug_collectives(self) -> dict:
+        """Collectives the group has issued (arx_debug_group_collectives)."""
+        out = (C.c_uint64 * 3)()
+        check(lib().arx_debug_group_collectives(self._g, out))
+        return {"histogram_allreduce": int(out[0]), "f64_allreduce": int(out[1]), "scene_broadcast": int(out[2])}
+
 
 class DeviceBuffer:
     """Device memory allocated through libarx (arx_device_alloc), so that a caller such as

@@ -305,12 +305,12 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
     ar_ms = allreduce_model_us(8, hist_bytes) / 1e3
     return {"frames": frames, "rays_per_gpu": shard, "p50_ms": float(np.percentile(a, 50)),
             "p99_ms": float(np.percentile(a, 99)), "max_ms": float(a.max()), "budget_ms": 1000.0 / 60.0,
-            "allreduce_model_ms": ar_ms, "p50_ms_with_allreduce": float(np.percentile(a, 50)) + ar_ms,
-            "max_ms_with_allreduce": float(a.max()) + ar_ms,
-            "allreduce_model": f"ring over 8 GPUs, {hist_bytes} B int64 histogram: 14 steps x 3 us + 1.75 x bytes "
-                               "at 153 GB/s (one xGMI link); the 8-GPU run's moving_listener measures it",
-            "per_frame": "one GPU's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra "
-                         "(projected 8-GPU rank) + the modelled all-reduce"}
+            "allreduce_ms_model": ar_ms,
+            "allreduce_model": f"NOT MEASURED: ring over 8 GPUs, {hist_bytes} B int64 histogram, 14 steps x 3 us + "
+                               "1.75 x bytes at 153 GB/s (one xGMI link); the latency fields above exclude it, the "
+                               "8-GPU run's moving_listener measures the real one",
+            "per_frame": "one GPU's 1/8 shard of a 1M-ray frame: re-place + trace + finalize + IR spectra, measured "
+                         "(the 8-GPU rank's frame without its all-reduce)"}
 
 
 def streaming_leg(m, audio, block: int) -> dict:
@@ -405,9 +405,10 @@ def main(argv=None) -> int:
     ap.add_argument("--frames-in-flight", type=int, choices=(1, 2, 3), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
-                         "too.  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 48 ms launches lose 5 %% "
-                         "to the overlap); 1 for N > 1 (the two-stream all-reduce order on one communicator has "
-                         "not run on a multi-GPU node yet)")
+                         "too.  Default at every N (so the 1..8-GPU lines compare like with like): 3 for c2, 2 for "
+                         "c3, 1 for c4 (its 48 ms launches lose 5 %% to the overlap).  Each frame's all-reduce runs "
+                         "on its own frame stream after the previous frame's (tests/test_gpu_collectives.py runs "
+                         "that chain with every collective forced on one GPU)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
     ap.add_argument("--process-group", action="store_true",
@@ -481,7 +482,7 @@ def main(argv=None) -> int:
             m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
 
     if args.frames_in_flight is None:
-        args.frames_in_flight = wl["fif"] if world == 1 else 1
+        args.frames_in_flight = wl["fif"]
     g.set_frames_in_flight(args.frames_in_flight)
     # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
     # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
@@ -569,7 +570,8 @@ def main(argv=None) -> int:
     td, td_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_td_c3.json")), args.workload, st0)
     vmem, vmem_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_vmem_ceiling.json")), args.workload, st0)
     conv_traffic = load_profile(os.path.join(PROFILES, "conv_traffic_r04j.json"))
-    conv_frames_s = world * frames / (conv_ms_max * 1e-3)
+    conv_frames_s = world * frames / (conv_ms_max * 1e-3)  # the convolution kernels' own window
+    conv_frames_step = world * frames * args.steps / elapsed  # the pipeline: frames convolved per timed step
     result = {
         "metric": METRIC,
         "value": value,
@@ -593,7 +595,11 @@ def main(argv=None) -> int:
             "ir_len": ir_len,
             "audio_frames_per_gpu": frames,
             "frames_in_flight": args.frames_in_flight,
-            "parallelism": (f"ray-shard x{world}, native RCCL int64 IR all-reduce (arx_group: "
+            "parallelism": (f"ray-shard x{world}, "
+                            + ("native RCCL int64 IR all-reduce per step" if world > 1 else
+                               "one rank: the group's RCCL communicator exists but arx_group_render skips its no-op "
+                               "IR all-reduce (arx_group.cpp; tests/test_gpu_collectives.py forces it on one GPU)")
+                            + " (arx_group: "
                             + ("one process, ncclCommInitAll over devices " + ",".join(map(str, plan["devices"]))
                                if plan["mode"] == "local" else f"one process per GPU, ncclCommInitRank, rank {rank}")
                             + ")"),
@@ -608,7 +614,13 @@ def main(argv=None) -> int:
         "ray_bounces_per_step": q_all,
         "nominal_ray_bounces_per_s": total_rays * wl["max_bounces"] * args.steps / elapsed,
         "receiver_hits_per_step_rank0": int(st0["receiver_hits"]),
-        "convolved_frames_per_s": conv_frames_s,
+        "convolved_frames_per_s": conv_frames_step,
+        "convolved_frames_per_s_kernel_window": conv_frames_s,
+        "convolved_frames_per_s_labels": {
+            "convolved_frames_per_s": "whole job, per timed step: stereo frames convolved (every GPU's copy of the "
+                                      "file) x K / the K steps' wall time, trace included",
+            "convolved_frames_per_s_kernel_window": "the same frames / the slowest GPU's IR-spectra + convolution "
+                                                    "window alone (the renderer's HIP events, arx_conv_times)"},
         "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms},
         "trace_kernel_build": {"vgprs": int(st0["trace_vgprs"]), "waves_per_simd": int(st0["trace_waves_per_simd"]),
                                "waves_target": int(st0["trace_waves_target"]),
@@ -622,11 +634,18 @@ def main(argv=None) -> int:
                           "kernel is co-limited by the vector-memory return path and VALU issue (roofline_td, "
                           "roofline_valu)",
             "binding_units": "td+valu",
+            "binding_unit": "td (the vector-memory return path, busy per CU-cycle; VALU issue per SIMD-cycle "
+                            "beside it in roofline_valu)",
+            "binding_frac": td["td_busy_per_cu_cycle"] if td else None,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic.get("bytes_per_launch") if traffic else None,
+            "traffic_GBps": traffic["bytes_per_launch"] / (trace_ms * 1e-3) / 1e9 if traffic else None,
+            "traffic_frac": traffic["bytes_per_launch"] / (trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "traffic_note": "the PMC-counted HBM bytes of one launch over its time, against the 8 TB/s peak: what "
+                            "actually crosses HBM (the tree and triangles sit in L2 / Infinity Cache)",
             "traffic_source": f"profiles/{PROFILES}/trace_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel "
                               "build, tree and workload; PMC counters cannot be read inside this run): " + traffic_why,
             "algorithmic_bytes_per_bounce": bpb,

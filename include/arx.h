@@ -315,6 +315,19 @@ arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames
 /* Same on device buffers (n_frames f64 in, 2*block_frames f64 out), no host synchronisation. */
 arx_status arx_stream_process_device(arx_stream* s, const double* d_in, size_t n_frames, double* d_out);
 
+/* Tests only: issue every collective of the group even at one rank -- the histogram all-reduce of
+ * arx_group_render (with frames in flight on every member's frame stream, chained by events), the
+ * f64 all-reduce of arx_group_allreduce_f64 and the rank path's scene broadcast of
+ * arx_group_set_scene -- so a one-GPU box runs the RCCL call paths a multi-GPU job takes.  out_of_place
+ * != 0: the all-reduces write separate receive buffers pre-filled with 0xFF (the histogram's is then
+ * copied back), so the result is right only if the collective moved the data.  Synchronises the
+ * members first.  ARX_ERR_INVALID_ARGUMENT for a group without a communicator (one GPU listed
+ * several times). */
+arx_status arx_debug_group_force_collectives(arx_group* g, int32_t on, int32_t out_of_place);
+/* Collectives the group has issued: out3[0] histogram all-reduces, [1] f64 all-reduces, [2] scene
+ * broadcasts (rank path). */
+arx_status arx_debug_group_collectives(const arx_group* g, uint64_t* out3);
+
 /* Debug / parity hooks. */
 arx_status arx_debug_ray_directions(uint64_t seed, uint64_t first_ray, uint64_t count, float* h_out_xyz,
                                     int device);

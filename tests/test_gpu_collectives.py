@@ -1,0 +1,128 @@
+"""GPU: every RCCL collective of a group, run on ONE GPU (arx_debug_group_force_collectives).
+
+A group of one rank normally skips its no-op collectives.  The 8-GPU node is the driver's, so the
+multi-GPU job's collective paths would first execute there; forcing them at one rank runs the same
+code on the one-GPU box:
+  * the histogram all-reduce of arx_group_render (ncclAllReduce int64 SUM on each frame's stream),
+    with one, two and three frames in flight -- the ev_reduced event chain that orders frame k + 1's
+    all-reduce after frame k's;
+  * arx_group_allreduce_f64 (sum and max), bench.py's barrier and max-over-ranks;
+  * the rank path's scene hand-over (size / flag / tree ncclBroadcast and ncclAllReduce over a
+    one-rank ncclCommInitRank communicator, arx_scene_share.hpp).
+A one-rank in-place all-reduce may launch nothing, so each is also run out of place: the receive
+buffer is pre-filled with 0xFF and the result is right only if the collective moved the data.
+Bar: IRs bit-identical to a plain renderer's (itself bit-exact vs the oracle, test_gpu_parity.py),
+values unchanged by a one-rank sum / max, the tree hash unchanged through the broadcast.
+"""
+import numpy as np
+import pytest
+
+from audiorenderingv2_amd import ArxError, AudioRenderer, RenderGroup, RenderSettings, receiver_local
+from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER
+from test_gpu_frames import FRAMES, S, bits, run_sequence
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def audio():
+    return (0.5 * np.sin(2 * np.pi * 440 * np.arange(3 * 16000 + 321) / 16000)).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def plain(conference, audio):
+    """The frame sequence on a plain renderer, one frame at a time."""
+    r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
+    try:
+        return run_sequence(r, [r], audio, 1)
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("out_of_place", [False, True])
+@pytest.mark.parametrize("fif", [1, 2, 3])
+def test_forced_histogram_allreduce_frames_in_flight(conference, audio, plain, fif, out_of_place):
+    g = RenderGroup(RenderSettings(**S), devices=[0], scene=conference, receiver=receiver_local())
+    try:
+        g.debug_force_collectives(True, out_of_place)
+        res = run_sequence(g, g.members, audio, fif)
+        n = g.debug_collectives()
+    finally:
+        g.close()
+    assert n["histogram_allreduce"] == len(FRAMES)
+    (o1, s1, ir1, st1), (o2, s2, ir2, st2) = plain, res
+    assert o1[0][0].any() and not o1[2][0].any()  # frames differ; the off-grid frame's IR is empty
+    for k, (a, b) in enumerate(zip(o1, o2)):
+        assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1])), f"frame {k}"
+    assert np.array_equal(bits(s1[0]), bits(s2[0])) and np.array_equal(bits(s1[1]), bits(s2[1]))
+    assert np.array_equal(bits(ir1[0]), bits(ir2[0])) and np.array_equal(bits(ir1[1]), bits(ir2[1]))
+    assert st1 == st2
+
+
+def test_unforced_group_of_one_skips_its_collectives(conference):
+    g = RenderGroup(RenderSettings(**S), devices=[0], scene=conference, receiver=receiver_local())
+    try:
+        g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+        g.render()
+        v = g.allreduce([1.0, 2.0])
+        assert np.array_equal(v, [1.0, 2.0])
+        assert g.debug_collectives() == {"histogram_allreduce": 0, "f64_allreduce": 0, "scene_broadcast": 0}
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("out_of_place", [False, True])
+def test_forced_f64_allreduce_sum_and_max(out_of_place):
+    g = RenderGroup(RenderSettings(rays=(4, 4, 4), sample_rate=16000), devices=[0])
+    try:
+        g.debug_force_collectives(True, out_of_place)
+        vals = np.array([0.0, -1.5, 3.25, 1e300, -7.0, np.pi], np.float64)
+        for op in ("sum", "max"):
+            out = g.allreduce(vals, op)
+            assert np.array_equal(out, vals), op  # one rank: the sum and the max of one value
+        # the bench's barrier / max-over-ranks timing shape: one value
+        assert g.allreduce([2.5], "max")[0] == 2.5
+        assert g.debug_collectives()["f64_allreduce"] == 3
+    finally:
+        g.close()
+
+
+def test_forced_rank_path_scene_broadcast(conference):
+    """A one-rank ncclCommInitRank group takes the rank path of arx_group_set_scene: rank 0 builds,
+    then size / flag / tree broadcasts and flag all-reduces over RCCL; the tree every rank holds has
+    the plain renderer's hash and renders the same IR."""
+    s = RenderSettings(rays=(60, 60, 10), sample_rate=16000, base_power=3.62, max_bounces=8, hrtf_absorption_rate=0.5)
+    r = AudioRenderer(s, scene=conference, receiver=receiver_local())
+    r.setEmitterPosInOptix(CONFERENCE_EMITTER)
+    r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+    r.render()
+    ref, rst = r.get_ir(), r.stats()
+    r.close()
+    for uid in (None, RenderGroup.unique_id()):
+        g = RenderGroup.rank(s, 1, 0, uid)
+        try:
+            g.debug_force_collectives(True, True)
+            g.set_receiver_model(*receiver_local())
+            g.set_scene(conference)
+            g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+            g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+            g.set_frames_in_flight(2)
+            g.render()
+            ir = g.get_ir()
+            st = g.stats()
+            n = g.debug_collectives()
+        finally:
+            g.close()
+        assert n == {"histogram_allreduce": 1, "f64_allreduce": 0, "scene_broadcast": 1}
+        assert st["tree_hash"] == rst["tree_hash"] and st["queries"] == rst["queries"]
+        assert np.array_equal(bits(ir[0]), bits(ref[0])) and np.array_equal(bits(ir[1]), bits(ref[1]))
+
+
+def test_force_refused_without_a_communicator():
+    g = RenderGroup(RenderSettings(rays=(4, 4, 4), sample_rate=16000), devices=[0, 0])
+    try:
+        with pytest.raises(ArxError):
+            g.debug_force_collectives(True)
+    finally:
+        g.close()
