@@ -413,8 +413,26 @@ struct GlobalStack {
     __device__ __forceinline__ void put(int sp, int v) const { base[(uint64_t)min(sp, nrows - 1) * stride] = v; }
 };
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, short stride = 0) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), stride, 0x7fffffff, 0x00020000);
+}
+
+#ifndef ARX_TRACE_IDXEN
+#define ARX_TRACE_IDXEN 1  // QNode2 loads indexed by node (idxen, a 32-B stride resource): no address VALU (C3 -1.6 %, profiles/r05/ab_idxen.txt); 0: byte offsets
+#endif
+typedef int arx_i32x4 __attribute__((ext_vector_type(4)));
+// buffer_load_dwordx4 ... idxen: address = base + vindex * stride + voffset + inst offset (the
+// hardware's structured-buffer addressing; clang has no builtin for it, the LLVM intrinsic is bound
+// by name as composable_kernel's amd_buffer_addressing.hpp does for the raw forms)
+__device__ arx_i32x4 arx_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                                                 int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+__device__ __forceinline__ uint4 node_half(__amdgpu_buffer_rsrc_t rs, int node, int half) {
+#if ARX_TRACE_IDXEN
+    const arx_i32x4 v = arx_struct_buffer_load_b128(rs, node, half * 16, 0, 0);
+    return make_uint4((uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w);
+#else
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, node * (int)sizeof(QNode2) + half * 16, 0, 0));
+#endif
 }
 
 // One branch-free node step: test both children of t.node, continue with the nearer hit child,
@@ -458,9 +476,8 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
             A = make_uint4(cached ? Al.x : Ag.x, cached ? Al.y : Ag.y, cached ? Al.z : Ag.z, cached ? Al.w : Ag.w);
             B = make_uint4(cached ? Bl.x : Bg.x, cached ? Bl.y : Bg.y, cached ? Bl.z : Bg.z, cached ? Bl.w : Bg.w);
         } else {
-            const int off = t.node * (int)sizeof(QNode2);
-            A = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-            B = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+            A = node_half(rs, t.node, 0);
+            B = node_half(rs, t.node, 1);
         }
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
         nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
@@ -756,7 +773,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
         stk.base = stk_lds + lane;
         stk_lds[lane] = -1;  // the dummy row under the stack (LdsStack::kSentinel)
     }
-    const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf) : (Q16 ? buffer_rsrc(a.qnodes) : buffer_rsrc(a.cnodes));
+    const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf)
+                                          : (Q16 ? buffer_rsrc(a.qnodes, ARX_TRACE_IDXEN ? (short)sizeof(QNode2) : (short)0)
+                                                 : buffer_rsrc(a.cnodes));
     const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
     const __amdgpu_buffer_rsrc_t trs = buffer_rsrc(tbase);
     const uint64_t n = a.ray_end - a.ray_begin;

@@ -36,7 +36,7 @@ class OrcStats(C.Structure):
 
 class OrcRayRecord(C.Structure):
     _fields_ = [("energy", C.c_float), ("distance", C.c_float), ("depth", C.c_int32), ("bin", C.c_int32),
-                ("queries", C.c_int32), ("last_tri", C.c_int32)]
+                ("queries", C.c_int32), ("last_tri", C.c_int32), ("path_hash", C.c_uint32)]
 
 
 _lib = None
@@ -189,9 +189,10 @@ class Scene:
     def records(self, p: OrcParams, first: int, count: int) -> np.ndarray:
         rec = (OrcRayRecord * count)()
         lib().orc_trace_records(C.byref(self.s), C.byref(p), first, count, rec)
-        return np.array([(r.energy, r.distance, r.depth, r.bin, r.queries, r.last_tri) for r in rec],
+        return np.array([(r.energy, r.distance, r.depth, r.bin, r.queries, r.last_tri, r.path_hash) for r in rec],
                         dtype=[("energy", np.float32), ("distance", np.float32), ("depth", np.int32),
-                               ("bin", np.int32), ("queries", np.int32), ("last_tri", np.int32)])
+                               ("bin", np.int32), ("queries", np.int32), ("last_tri", np.int32),
+                               ("path_hash", np.uint32)])
 
 
 def finalize_ir(p: OrcParams, L: np.ndarray, R: np.ndarray):

@@ -8,11 +8,13 @@ rays four ways (arx_oracle.h `arith`):
   2  IEEE with the reflection about normalize(cr) as the reference writes it (devicePrograms.cu:77,
      173) -- the convention before round 3, to price the reflection about cr on its own,
   and mode 0 on seed 2: the Monte-Carlo spread between two runs of the clock-seeded reference.
-Per ray it keeps the final record, so beside the IR's relative RMS it reports how many rays take a
-different path and the relative RMS over the rays whose path agrees (oracle/pricing.py); the bars of
-DESIGN.md section 3 are evaluated per config.
+Per ray it keeps the final record (its closest-hit triangle sequence hashed), so every ray is classed
+as identical, same path with a bin flip (roundf((dist / 343) * sr) on the other side of a .5
+boundary), or diverged (another path), and each class's share of the IR's per-bin relative RMS is
+reported beside the bin-tolerant RMS of the same-path rays (oracle/pricing.py); the bars of DESIGN.md
+section 3 are evaluated per config (round 5).
 
-    python tools/arith_pricing.py [--out profiles/r04/ieee_vs_reference_arith.json]
+    python tools/arith_pricing.py [--out profiles/r05/ieee_vs_reference_arith.json]
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 import pyoracle as po  # noqa: E402
-from pricing import bars_met, compare, records  # noqa: E402
+from pricing import BARS, BIN_FLIP_DX, OTHER_PATH_VS_REFERENCE_FORM, bars_met, compare, records  # noqa: E402
 from audiorenderingv2_amd import place_receiver_vertices, receiver_local  # noqa: E402
 from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER, conference_standin  # noqa: E402
 
@@ -53,7 +55,7 @@ def world():
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r04", "ieee_vs_reference_arith.json"))
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r05", "ieee_vs_reference_arith.json"))
     ap.add_argument("--c3-rays", type=int, default=1_000_000)
     ap.add_argument("--c4-begin", type=int, default=5_000_000)
     ap.add_argument("--c4-rays", type=int, default=1_000_000)
@@ -66,6 +68,8 @@ def main(argv=None) -> int:
            "modes": {"0": "build IEEE (reflection about cr)", "1": "reference fast-math arithmetic",
                      "2": "IEEE, reflection about normalize(cr)", "seed2": "mode 0 on seed 2 (Monte-Carlo spread)"},
            "configs": {}}
+    res["bars_defined"] = {"fixed": BARS, "bin_flip_dx": BIN_FLIP_DX,
+                           "other_path_vs_reference_form": OTHER_PATH_VS_REFERENCE_FORM}
     if os.path.exists(args.out):  # keep the configs not re-run
         with open(args.out) as f:
             res["configs"] = json.load(f).get("configs", {})
@@ -82,13 +86,14 @@ def main(argv=None) -> int:
                                hrtf=HRTF, emitter=CONFERENCE_EMITTER, listener=CONFERENCE_LISTENER, arith=arith,
                                seed=seed)
             recs[key] = records(osc, p, begin, end, args.threads)
-        cmp = lambda a, b: compare(recs[a], recs[b], ta, ir_len, c["sr"], HRTF)  # noqa: E731
+        arith = {0: 0, 1: 1, 2: 2, "seed2": 0}
+        cmp = lambda a, b: compare(recs[a], recs[b], ta, ir_len, c["sr"], HRTF, arith[a], arith[b])  # noqa: E731
         r = {"rays": [begin, end], "launch_rays": n, "bounces": c["bounces"], "sample_rate": c["sr"],
              "ieee_vs_reference": cmp(0, 1),
              "normalize_reflection_vs_reference": cmp(2, 1),
              "ieee_vs_normalize_reflection": cmp(0, 2),
              "seed1_vs_seed2": cmp(0, "seed2")}
-        r["bars"] = bars_met(r["ieee_vs_reference"], r["seed1_vs_seed2"])
+        r["bars"] = bars_met(r["ieee_vs_reference"], r["seed1_vs_seed2"], r["normalize_reflection_vs_reference"])
         r["bars_normalize_reflection"] = bars_met(r["normalize_reflection_vs_reference"], r["seed1_vs_seed2"])
         r["cpu_s"] = round(time.time() - t0, 1)
         res["configs"][name] = r

@@ -58,7 +58,7 @@ static bool slab(const float lo[3], const float hi[3], const Q& q, float tmax, f
 }
 
 struct Stats {
-    double visits = 0, tests = 0, leaves = 0, maxstack = 0;
+    double visits = 0, tests = 0, leaves = 0, maxstack = 0, skips2 = 0;
     double shallow[8] = {};  // visits to nodes at depth <= 2 + k below the top node
     double nhit[9] = {};     // visits by number of children hit
 };
@@ -107,14 +107,49 @@ static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Sta
     std::vector<std::pair<float, int>> stack;  // (tn, code) ; code >= 0 node, < 0 leaf
     stack.push_back({0.0f, 0});
     size_t maxs = 0;
+    bool after_leaf = false, continue_culling = false;
     while (!stack.empty()) {
-        auto [tn0, code] = stack.back();
+        auto [tn0, code] = stack.back();  // (copies: DEPTH2 may replace them)
         stack.pop_back();
         static const bool nocull = std::getenv("NOCULL") != nullptr;  // the GPU stack keeps no distances
-        if (tn0 > best && !nocull) continue;
+        // QCULL=k: the kernel's packed stack word (round 5) -- the entry distance kept as a 7-bit
+        // lower bound floor(tn * 2^k) (saturating at 127), a pop culled when that bound exceeds the
+        // best hit; DEPTH2=1: only the two topmost entries are looked at per pop (a culled top is
+        // replaced by the one below it, which is taken unchecked)
+        static const int qcull = std::getenv("QCULL") ? std::atoi(std::getenv("QCULL")) : -1;
+        static const bool depth2 = std::getenv("DEPTH2") != nullptr;
+        // LEAFCULL=1: pops are checked only right after a leaf (where the best hit changes), and
+        // there as many as are culled; a node step's own pop is taken unchecked
+        static const bool leafcull = std::getenv("LEAFCULL") != nullptr;
+        const bool check = !leafcull || after_leaf;
+        after_leaf = false;
+        if (qcull >= 0 && leafcull) {
+            auto key = [&](float tn) { return std::min(255.0f, std::floor(tn * std::ldexp(1.0f, qcull))); };
+            auto culled = [&](float tn) { return key(tn) > std::floor(best * std::ldexp(1.0f, qcull)); };
+            if (check && culled(tn0)) continue_culling = true;
+            if (continue_culling) {
+                if (culled(tn0)) continue;
+                continue_culling = false;
+            }
+        } else if (qcull >= 0) {
+            auto key = [&](float tn) { return std::min(127.0f, std::floor(tn * std::ldexp(1.0f, qcull))); };
+            auto culled = [&](float tn) { return key(tn) > std::floor(best * std::ldexp(1.0f, qcull)); };
+            if (culled(tn0)) {
+                if (!depth2) continue;
+                if (stack.empty()) break;
+                auto nx = stack.back();
+                stack.pop_back();
+                tn0 = nx.first;
+                code = nx.second;
+                st.skips2 += 1;
+            }
+        } else if (tn0 > best && !nocull) {
+            continue;
+        }
         if (code < 0) {
             const int v = -code - 1, first = v >> 4, cnt = v & 15;
             st.leaves += 1;
+            after_leaf = true;
             for (int k = 0; k < cnt; ++k) {
                 st.tests += 1;
                 float tt;
