@@ -118,6 +118,8 @@ SIGNATURES = {
     "arx_set_ir_device": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_size_t]),
     "arx_convolute_audio_file": (C.c_int, [_P, _F, C.c_size_t, _F, _F, _D, _D]),
     "arx_convolute_device": (C.c_int, [_P, _P, C.c_size_t, _P, _P]),
+    "arx_convolute_prepare_input": (C.c_int, [_P, _P, C.c_size_t]),
+    "arx_convolute_prepared": (C.c_int, [_P, _P, _P, C.POINTER(C.c_size_t)]),
     "arx_convolute_live_block": (C.c_int, [_P, _D, C.c_size_t, _D, C.c_size_t]),
     "arx_convolute_live_device": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "arx_prepare_ir_spectra": (C.c_int, [_P, C.c_int]),

@@ -1498,6 +1498,39 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     return fif_done_conv(r);
 }
 
+arx_status arx_convolute_prepare_input(arx_renderer* r, const float* d_in, size_t n_frames) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (n_frames > 0 && !d_in) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = fif_wait_conv(r);  // the plan's scratch is shared with the other frame in flight
+    if (st == ARX_OK) st = ensure_conv(r, false);
+    if (st != ARX_OK) return st;
+    ARX_HIP(conv_prepare_input(r->conv, d_in, (int64_t)n_frames, r->stream));
+    return fif_done_conv(r);
+}
+
+arx_status arx_convolute_prepared(arx_renderer* r, float* d_out_left, float* d_out_right, size_t* n_frames) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    if (!r->conv || !conv_has_prepared(r->conv))
+        return fail(ARX_ERR_NOT_READY, "no prepared input (arx_convolute_prepare_input; another file convolution on "
+                                       "this renderer discards it)");
+    const int64_t n = conv_prepared_frames(r->conv);
+    if (n > 0 && (!d_out_left || !d_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    ARX_HIP(hipSetDevice(r->cfg.device));
+    arx_status st = fif_wait_conv(r);
+    if (st != ARX_OK) return st;
+    const bool ir_new = r->conv_ir_dirty;
+    const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
+    ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
+    ARX_HIP(conv_run_prepared(r->conv, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
+                              ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
+    r->conv_ir_dirty = false;
+    ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
+    ++r->conv_launches;
+    if (n_frames) *n_frames = (size_t)n;
+    return fif_done_conv(r);
+}
+
 arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t in_bytes, float* h_out_left,
                                     float* h_out_right, double* conv_ms, double* proc_ms) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");

@@ -65,6 +65,14 @@ struct ConvPlan {
     double2* d_S = nullptr;      // scratch spectra: pairs_cap * 3 * M (shared + 2 channels)
     double* d_Y = nullptr;       // per block, per channel M*lin (length n + sr - 1)
     int64_t pairs_cap = 0;
+    // input reuse (conv_prepare_input): the prepared file's length, and where its spectra live --
+    // S[pair][0] on the direct path with the chained pass C, else a copy of the input (d_prep_in)
+    // that conv_run_prepared convolves in full
+    bool prepared = false;
+    bool prep_spectra = false;
+    int64_t prep_frames = 0;
+    float* d_prep_in = nullptr;
+    size_t prep_cap = 0;
     char desc[160] = {0};
 };
 
@@ -401,7 +409,8 @@ __global__ __launch_bounds__(kThreads) void pass_b(PassArgs a) {
     const int k1 = blockIdx.x;
     const int64_t batch = blockIdx.y;
     const int N2 = a.N2;
-    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
+    constexpr bool kMul = MODE == 0 || MODE == 4;  // multiply by H and invert
+    double2* row = (MODE == 1) ? a.H + (size_t)batch * a.M + (int64_t)k1 * N2 : a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
     double2* twl = lds + N2;  // W_N2^e staged in LDS (see pass A)
     for (int i = threadIdx.x; i < N2; i += kThreads) {
         lds[i] = row[i];
@@ -1010,7 +1019,10 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
 }
 
 // Pass B: per row k1 (one wave; nt / 64 rows per block): forward row FFT (N2); mode 1 stores it (IR
-// spectrum); mode 0 multiplies by H_c, inverse row FFT, * W_n^(-n2 k1), for both channels.
+// spectrum); mode 0 multiplies by H_c, inverse row FFT, * W_n^(-n2 k1), for both channels.  Input
+// reuse (conv_prepare_input / conv_run_prepared): mode 3 stores the forward row FFT of an audio
+// block pair in place (S[pair][0] becomes the pair's full spectrum X), mode 4 is mode 0 on such an
+// X (no forward FFT) -- the same arithmetic as mode 0 in two launches, so the outputs are identical.
 // LDS: 2 x N2 per row (the spectrum; H_0's row, then the product), W_N2 (N2) -- small enough for
 // 3 blocks per CU, so one round of blocks covers the C3 grid.
 template <int MODE, bool R7, int LM, int L2>
@@ -1031,7 +1043,8 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     double2* work = spec + N2;
     double2* tw2 = lds + (size_t)rows * 2 * N2;
     const bool live = k1 < N1;
-    double2* row = (MODE == 0) ? a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2 : a.H + (size_t)batch * a.M + (int64_t)k1 * N2;
+    constexpr bool kMul = MODE == 0 || MODE == 4;  // multiply by H and invert
+    double2* row = (MODE == 1) ? a.H + (size_t)batch * a.M + (int64_t)k1 * N2 : a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
     // every global operand of the row up front: the row, H_0 and H_1's rows and the four-step
     // twiddles, so the wave's only global round trip before its stores is this one
     // W_n^(n2 k1) = W_N1^q W_n^r with n2 k1 = q N2 + r (as in pass A): two small tables that stay in
@@ -1043,7 +1056,7 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
     for (int it = 0; it < IT; ++it) {
         const int i = j + 64 * it;
         const bool in = live && i < N2;
-        const bool in0 = MODE == 0 && in;
+        const bool in0 = kMul && in;
         v[it] = in ? row[i] : make_double2(0.0, 0.0);
         h[it] = in0 ? a.H[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
         h1[it] = in0 ? a.H[(size_t)a.M + (int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
@@ -1062,13 +1075,13 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
         const int i = j + 64 * it;
         if (live && i < N2) {
             spec[i] = v[it];
-            if (MODE == 0) work[i] = h[it];
+            if (kMul) work[i] = h[it];
         }
     }
     __syncthreads();
     if (!live) return;  // no block barrier below
-    fft_wave_any<R7, LM, L2>(spec, tw2, m.f2, j, -1);
-    if (MODE == 1) {
+    if (MODE != 4) fft_wave_any<R7, LM, L2>(spec, tw2, m.f2, j, -1);
+    if (MODE == 1 || MODE == 3) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int i = j + 64 * it;
@@ -1112,7 +1125,9 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
 // transforms its S row and its G row (interleaved), reads its mirror's G row from LDS, and goes on
 // as pass_b_mr<0>.  Block pair 0 also stores H_L / H_R, the spectra later calls reuse.
 // LDS: 2 x N2 per wave (S's spectrum; G's row, then the product), W_N2 (N2).
-template <bool R7, int LM, int L2>
+// XS (input reuse, conv_run_prepared): the S rows already hold the block pairs' row spectra (pass_b_mr
+// mode 3), so only the G rows are transformed forward.
+template <bool R7, int LM, int L2, bool XS>
 __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -1163,7 +1178,10 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     }
     __syncthreads();
     CONV_PROF_MARK(1);
-    fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
+    if constexpr (XS)
+        fft_wave_any<R7, LM, L2>(gbuf, tw2, m.f2, j, -1);
+    else
+        fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
     __syncthreads();  // the mirror row's G spectrum is complete
     double2 h0[IT], h1[IT];
 #pragma unroll
@@ -1492,6 +1510,7 @@ ConvPlan* conv_plan_create(int32_t ir_len, int32_t sample_rate, int device, char
 
 void conv_plan_destroy(ConvPlan* p) {
     if (!p) return;
+    hipFree(p->d_prep_in);
     hipFree(p->d_tw);
     hipFree(p->d_H);
     hipFree(p->d_G);
@@ -1555,11 +1574,11 @@ static size_t mr_lds_a(const ConvPlan* p, int tc) {
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
-template <bool R7, int LM, int L2>
+template <bool R7, int LM, int L2, bool XS = false>
 static void launch_b_pair(const ConvPlan* p, int batches, MrArgs m, hipStream_t s) {
     const unsigned units8 = (unsigned)((p->N1 + 1) / 2 + 7) / 8 * 8;  // see pass_b_pair's XCD mapping
     m.batches = batches;
-    hipLaunchKernelGGL((pass_b_pair<R7, LM, L2>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2), s, m);
+    hipLaunchKernelGGL((pass_b_pair<R7, LM, L2, XS>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2), s, m);
 }
 template <int MODE, bool R7, int LM, int L2>
 static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipStream_t s) {
@@ -1594,6 +1613,8 @@ static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
 #define ARX_CONV_CHAIN 2
 #endif
 template <bool R7, int LM, int L1, int L2>
+static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipStream_t s);
+template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
     hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)(pairs + (with_ir ? 1 : 0))),
@@ -1602,6 +1623,39 @@ static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool wi
         launch_b_pair<R7, LM, L2>(p, (int)pairs, m, s);
     else
         launch_b_mr<0, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
+    mr_pass_c<R7, LM, L1, L2>(p, a, pairs, s);
+}
+
+// Input reuse, step 1 (conv_prepare_input): the audio's columns (pass A) and forward rows (pass B
+// mode 3) once; S[pair][0] keeps every block pair's spectrum.
+template <bool R7, int LM, int L1, int L2>
+static void mr_prepare(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipStream_t s) {
+    MrArgs m = mr_args(p, a);
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)pairs), dim3(64 * ARX_CONV_TCA),
+                       mr_lds_a(p, ARX_CONV_TCA), s, m);
+    launch_b_mr<3, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
+}
+
+// Input reuse, step 2 (conv_run_prepared): a new IR's columns alone in pass A (one batch, to G), then
+// pass B without the audio's forward rows (pass_b_pair<XS> with a new IR, mode 4 without), then pass C.
+template <bool R7, int LM, int L1, int L2>
+static void mr_prepared(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
+    MrArgs m = mr_args(p, a);
+    if (with_ir) {
+        MrArgs mi = m;
+        mi.p.n_pairs = 0;  // batch 0 of this launch is the IR (pass_a_mr mode 0's batch past the pairs)
+        hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), 1u), dim3(64 * ARX_CONV_TCA),
+                           mr_lds_a(p, ARX_CONV_TCA), s, mi);
+        launch_b_pair<R7, LM, L2, true>(p, (int)pairs, m, s);
+    } else {
+        launch_b_mr<4, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
+    }
+    mr_pass_c<R7, LM, L1, L2>(p, a, pairs, s);
+}
+
+template <bool R7, int LM, int L1, int L2>
+static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipStream_t s) {
+    MrArgs m = mr_args(p, a);
     if (p->n == 2 * p->sr && p->N1 % 2 == 0) {  // inverse columns and seams in one pass
         m.chain = ARX_CONV_CHAIN;
         const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
@@ -1690,6 +1744,7 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
         return conv_run(p, d_in, n_frames, d_out_left, d_out_right, nullptr, nullptr, s);
     }
     if (n_frames <= 0) return hipSuccess;
+    p->prepared = false;  // any other file convolution discards a prepared input (pass A overwrites its spectra)
     const int64_t S = n_frames / p->sr;  // kernels.cu:413
     if (S == 0) {  // nothing convolved: the reference output stays zero
         hipError_t e = hipMemsetAsync(d_out_left, 0, (size_t)n_frames * sizeof(float), s);
@@ -1740,6 +1795,113 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
         hipLaunchKernelGGL(pass_c, dim3(p->N2 / p->tc, (unsigned)(2 * pairs)), dim3(kThreads), lds_a, s, a);
     }
     hipLaunchKernelGGL(pass_d, dim3((unsigned)((n_frames + kThreads - 1) / kThreads), 2), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// Input reuse (the reference's re-render pattern: full_render_cycle convolves the same file with
+// every new IR, AudioRenderer.cpp:790-798, main.cpp:40-67).  conv_prepare_input transforms the file's
+// block pairs once (pass A + forward rows, S[pair][0] keeps the spectra); conv_run_prepared then costs
+// a new IR's spectra (its columns alone in pass A, its rows in pass B), the products and the inverse
+// rows (pass B, no forward FFT of the audio) and pass C.  Same arithmetic as conv_run in the same
+// order, so the output is bit-identical.  Plans without the chained pass C keep a copy of the input
+// and convolve it in full.
+static bool reuse_spectra(const ConvPlan* p) { return p->direct && p->n == 2 * p->sr && p->N1 % 2 == 0; }
+
+static hipError_t ensure_scratch(ConvPlan* p, int64_t pairs) {
+    if (pairs <= p->pairs_cap && p->d_S) return hipSuccess;
+    hipFree(p->d_S);
+    hipFree(p->d_Y);
+    p->d_S = nullptr;
+    p->d_Y = nullptr;
+    p->pairs_cap = 0;
+    p->prepared = false;
+    const hipError_t e = hipMalloc(&p->d_S, (size_t)pairs * 3 * p->M * sizeof(double2));
+    if (e == hipSuccess) p->pairs_cap = pairs;
+    return e;
+}
+
+hipError_t conv_prepare_input(ConvPlan* p, const float* d_in, int64_t n_frames, hipStream_t s) {
+    p->prepared = false;
+    p->prep_frames = n_frames > 0 ? n_frames : 0;
+    p->prep_spectra = reuse_spectra(p);
+    const int64_t S = p->prep_frames / p->sr, pairs = (S + 1) / 2;
+    (void)hipGetLastError();
+    if (!p->prep_spectra) {  // keep the samples: conv_run_prepared convolves them in full
+        if ((size_t)p->prep_frames > p->prep_cap) {
+            hipFree(p->d_prep_in);
+            p->d_prep_in = nullptr;
+            p->prep_cap = 0;
+            const hipError_t e = hipMalloc(&p->d_prep_in, (size_t)p->prep_frames * sizeof(float));
+            if (e != hipSuccess) return e;
+            p->prep_cap = (size_t)p->prep_frames;
+        }
+        if (p->prep_frames > 0) {
+            const hipError_t e = hipMemcpyAsync(p->d_prep_in, d_in, (size_t)p->prep_frames * sizeof(float),
+                                                hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return e;
+        }
+        p->prepared = true;
+        return hipSuccess;
+    }
+    if (S > 0) {
+        hipError_t e = ensure_scratch(p, pairs);
+        if (e != hipSuccess) return e;
+        PassArgs a = base_args(p);
+        a.in = d_in;
+        a.S = p->d_S;
+        a.n_blocks = S;
+        a.n_pairs = pairs;
+        a.len = p->prep_frames;
+        mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
+            mr_prepare<decltype(r7)::value, decltype(lm)::value, decltype(l1)::value, decltype(l2)::value>(p, a, pairs, s);
+        });
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    p->prepared = true;
+    return hipSuccess;
+}
+
+bool conv_has_prepared(const ConvPlan* p) { return p && p->prepared; }
+int64_t conv_prepared_frames(const ConvPlan* p) { return p && p->prepared ? p->prep_frames : 0; }
+
+hipError_t conv_run_prepared(ConvPlan* p, float* d_out_left, float* d_out_right, const float* d_ir_left,
+                             const float* d_ir_right, hipStream_t s) {
+    if (!p->prepared) return hipErrorInvalidValue;
+    const int64_t n_frames = p->prep_frames;
+    if (!p->prep_spectra) {
+        const hipError_t e = conv_run(p, p->d_prep_in, n_frames, d_out_left, d_out_right, d_ir_left, d_ir_right, s);
+        p->prepared = true;  // conv_run above reads the kept copy; nothing of it is overwritten
+        return e;
+    }
+    const bool with_ir = d_ir_left && d_ir_right;
+    const int64_t S = n_frames / p->sr;
+    if (S == 0) {  // no block: the output stays zero (kernels.cu:413), the IR spectra still follow the IR
+        if (with_ir) {
+            const hipError_t e = conv_set_ir(p, d_ir_left, d_ir_right, s);
+            if (e != hipSuccess) return e;
+        }
+        if (n_frames <= 0) return hipSuccess;
+        hipError_t e = hipMemsetAsync(d_out_left, 0, (size_t)n_frames * sizeof(float), s);
+        if (e == hipSuccess) e = hipMemsetAsync(d_out_right, 0, (size_t)n_frames * sizeof(float), s);
+        return e;
+    }
+    const int64_t pairs = (S + 1) / 2;
+    (void)hipGetLastError();
+    PassArgs a = base_args(p);
+    a.S = p->d_S;
+    a.n_blocks = S;
+    a.n_pairs = pairs;
+    a.len = n_frames;
+    a.out_l = d_out_left;
+    a.out_r = d_out_right;
+    a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
+    a.ir_l = d_ir_left;
+    a.ir_r = d_ir_right;
+    mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
+        mr_prepared<decltype(r7)::value, decltype(lm)::value, decltype(l1)::value, decltype(l2)::value>(p, a, pairs,
+                                                                                                      with_ir, s);
+    });
     return hipGetLastError();
 }
 

@@ -88,6 +88,14 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
                     const float* d_ir_left, const float* d_ir_right, hipStream_t s);
 const char* conv_plan_describe(const ConvPlan* p);
+// Input reuse: conv_prepare_input transforms a file's blocks once (kept in the plan until the next
+// conv_run or conv_prepare_input); conv_run_prepared convolves them with the current IR (new spectra
+// from d_ir_left / d_ir_right when given), bit-identical to conv_run on the same input.
+hipError_t conv_prepare_input(ConvPlan* p, const float* d_in, int64_t n_frames, hipStream_t s);
+hipError_t conv_run_prepared(ConvPlan* p, float* d_out_left, float* d_out_right, const float* d_ir_left,
+                             const float* d_ir_right, hipStream_t s);
+bool conv_has_prepared(const ConvPlan* p);
+int64_t conv_prepared_frames(const ConvPlan* p);
 // Live (mic) block: plans created with sample_rate = block length.  One block of n_in <= block
 // f64 samples, circular length-ir_len convolution with both IR spectra, / (ir_len/2), zipped
 // L/R into 2*ir_len doubles (AudioRenderer.cpp:593-651, kernels.cu:345-377, 450-487).

@@ -317,6 +317,18 @@ class AudioRenderer:
         check(lib().arx_convolute_device(self._h, C.c_void_p(d_in), n_frames, C.c_void_p(d_out_left),
                                          C.c_void_p(d_out_right)))
 
+    def convolute_prepare_input(self, d_in: int, n_frames: int) -> None:
+        """arx_convolute_prepare_input: the file's blocks transformed once, for convolute_prepared
+        (the reference re-convolves the same file with every new IR, AudioRenderer.cpp:790-798)."""
+        check(lib().arx_convolute_prepare_input(self._h, C.c_void_p(d_in), n_frames))
+
+    def convolute_prepared(self, d_out_left: int, d_out_right: int) -> int:
+        """arx_convolute_prepared: the prepared file convolved with the current IR (bit-identical to
+        convolute_device on the same input); returns the frame count."""
+        n = C.c_size_t()
+        check(lib().arx_convolute_prepared(self._h, C.c_void_p(d_out_left), C.c_void_p(d_out_right), C.byref(n)))
+        return int(n.value)
+
 
 class LiveStream:
     """Streaming convolution of a renderer's IR (arx_stream_*, uniformly partitioned overlap-save

@@ -402,6 +402,7 @@ def main(argv=None) -> int:
     ap.add_argument("--c5-frames", type=int, default=600,
                     help="moving-listener frames after the timed steps (SURVEY C5); 0 disables")
     ap.add_argument("--no-streaming", action="store_true")
+    ap.add_argument("--no-reuse", action="store_true", help="skip the input-reuse convolution leg")
     ap.add_argument("--frames-in-flight", type=int, choices=(1, 2, 3), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
@@ -548,6 +549,39 @@ def main(argv=None) -> int:
         conv_ms_all.append(float(np.mean(cl)))
     conv_ms = conv_ms_all[0]
     conv_ms_max = ranks.max(max(conv_ms_all))
+    # Input reuse (arx_convolute_prepare_input / _prepared): the reference re-convolves the same file
+    # with every new IR (full_render_cycle, AudioRenderer.cpp:790-798), so the file's blocks can be
+    # transformed once.  Its own leg, one frame in flight, never the headline's work: the same steps
+    # with the convolution of the prepared input, its kernel window beside the full one.
+    reuse = None
+    if not args.no_reuse:
+        g.set_frames_in_flight(1)
+        for m, (x, _, _) in zip(members, bufs):
+            m.convolute_prepare_input(x.ptr, frames)
+
+        def step_reuse():
+            g.render(timed=False)
+            for m, (_, ol, orr) in zip(members, bufs):
+                m.convolute_prepared(ol.ptr, orr.ptr)
+
+        for _ in range(args.warmup):
+            step_reuse()
+        g.synchronize()
+        ranks.barrier()
+        t0r = time.perf_counter()
+        for _ in range(args.steps):
+            step_reuse()
+        g.synchronize()
+        ranks.barrier()
+        elr = ranks.max(time.perf_counter() - t0r)
+        reuse_ms = float(np.mean(m0.conv_times(args.steps)))
+        reuse = {"conv_ms_rank0": reuse_ms, "ms_per_step": elr / args.steps * 1e3,
+                 "convolved_frames_per_s_kernel_window": frames / (reuse_ms * 1e-3),
+                 "why": "the reference's re-render pattern (the same file, a new IR every frame): the file's blocks "
+                        "transformed once (arx_convolute_prepare_input), each step's convolution "
+                        "(arx_convolute_prepared) = the new IR's spectra + products + inverse transforms, "
+                        "bit-identical to the full one (tests/test_gpu_conv_reuse.py); not the headline's work"}
+        g.set_frames_in_flight(args.frames_in_flight)
 
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
     moving = None
@@ -622,6 +656,7 @@ def main(argv=None) -> int:
             "convolved_frames_per_s_kernel_window": "the same frames / the slowest GPU's IR-spectra + convolution "
                                                     "window alone (the renderer's HIP events, arx_conv_times)"},
         "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms},
+        "convolution_input_reuse": reuse,
         "trace_kernel_build": {"vgprs": int(st0["trace_vgprs"]), "waves_per_simd": int(st0["trace_waves_per_simd"]),
                                "waves_target": int(st0["trace_waves_target"]),
                                "node_format": NODE_FORMATS.get(int(st0["trace_format"]), str(st0["trace_format"])),

@@ -275,6 +275,16 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
 /* Same on device-resident buffers (n_frames floats each); no host synchronisation. */
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
                                 float* d_out_right);
+/* Input reuse for the reference's re-render pattern: full_render_cycle (AudioRenderer.cpp:790-798,
+ * called by main.cpp:40-67 on every listener move) convolves the SAME file with every new IR.
+ * arx_convolute_prepare_input transforms the file's one-second blocks once (device input, n_frames
+ * samples; the input buffer may be reused by the caller afterwards); arx_convolute_prepared then
+ * convolves them with the renderer's current IR into the caller's device outputs (n_frames each,
+ * *n_frames set when non-NULL) -- bit-identical to arx_convolute_device on the same input, without
+ * the input's forward transform.  The prepared input stays until the next arx_convolute_device /
+ * arx_convolute_audio_file / arx_convolute_prepare_input on this renderer (ARX_ERR_NOT_READY after). */
+arx_status arx_convolute_prepare_input(arx_renderer* r, const float* d_in, size_t n_frames);
+arx_status arx_convolute_prepared(arx_renderer* r, float* d_out_left, float* d_out_right, size_t* n_frames);
 
 /* AudioRenderer::convoluteLiveInput (AudioRenderer.h:29; AudioRenderer.cpp:593-661) over
  * convoluteFromLiveInput (kernels.cu:345-377) minus the CircularBuffer (which stays with the
