@@ -239,16 +239,6 @@ void receiver_bound(const arx_renderer* r, float lo[3], float hi[3], bool* empty
 // offsets and num_records 0x7fffffff (arx_trace.hip buffer_rsrc; a load past it returns zeros, which
 // the leaf step uses for idle lanes): every record must end below 2^31 bytes, or a triangle would read
 // back as zeros (det 0, a silently dropped hit).  44.7 M triangle records / 33.5 M coded nodes.
-arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris) {
-    constexpr uint64_t kMax = 0x7fffffffull;
-    if ((uint64_t)n_tris * sizeof(TriRec) > kMax)
-        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu triangle records x %zu B exceed the trace kernel's "
-                    "31-bit buffer offsets", (unsigned long long)n_tris, sizeof(TriRec));
-    if ((uint64_t)n_nodes * sizeof(BvhNode) > kMax)
-        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu BVH nodes x %zu B exceed the trace kernel's "
-                    "31-bit buffer offsets", (unsigned long long)n_nodes, sizeof(BvhNode));
-    return ARX_OK;
-}
 
 // Frames in flight (no-ops with one): the current set's stream waits for every other set's last
 // trace / for the set that did the last step of a chain (convolutions, all-reduces, scene writes),
@@ -1768,3 +1758,15 @@ arx_status arx_stream_process(arx_stream* s, const double* h_in, size_t n_frames
 }
 
 }  // extern "C"
+
+// (declared in arx_internal.hpp: arx_group.cpp checks a rank-0 build before broadcasting it)
+arx_status arx::check_buffer_offsets(size_t n_nodes, size_t n_tris) {
+    constexpr uint64_t kMax = 0x7fffffffull;
+    if ((uint64_t)n_tris * sizeof(TriRec) > kMax)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu triangle records x %zu B exceed the trace kernel's "
+                    "31-bit buffer offsets", (unsigned long long)n_tris, sizeof(TriRec));
+    if ((uint64_t)n_nodes * sizeof(BvhNode) > kMax)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "scene too large: %llu BVH nodes x %zu B exceed the trace kernel's "
+                    "31-bit buffer offsets", (unsigned long long)n_nodes, sizeof(BvhNode));
+    return ARX_OK;
+}

@@ -289,6 +289,9 @@ arx_status share_scene(Chan& ch, int32_t rank, const float* tri_v, const float* 
                 img = build_scene_image(tri_v, tri_abs, n);
                 if (!img) root_st = fail(ARX_ERR_OUT_OF_MEMORY, "scene build failed");
             }
+            // a tree beyond the trace kernel's buffer offsets fails here, on every rank, before its
+            // image is staged and broadcast (every rank's set_scene_image would reject it anyway)
+            if (root_st == ARX_OK) root_st = check_buffer_offsets(1 + img->bvh.nodes.size(), img->bvh.tris.size());
             if (root_st != ARX_OK) {
                 root_err = arx_last_error();
                 return false;

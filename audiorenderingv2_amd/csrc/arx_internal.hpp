@@ -69,6 +69,9 @@ using SceneRef = std::shared_ptr<const SceneImage>;
 
 // Input checks of arx_set_scene (finite vertices, absorption in [0, 1] or the receiver marks).
 arx_status check_scene_input(const float* tri_v, const float* tri_abs, int64_t n);
+// The trace kernel's 31-bit buffer offsets: a tree of n_nodes coded nodes and n_tris triangle records
+// must fit them (ARX_ERR_INVALID_ARGUMENT otherwise).
+arx_status check_buffer_offsets(size_t n_nodes, size_t n_tris);
 // One host build (counted by arx_scene_build_count).
 SceneRef build_scene_image(const float* tri_v, const float* tri_abs, int64_t n);
 // Byte image of a build for the rank path's RCCL broadcast, and its inverse (NULL + why on a

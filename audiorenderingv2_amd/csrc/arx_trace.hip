@@ -417,6 +417,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, sho
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), stride, 0x7fffffff, 0x00020000);
 }
 
+// lanes in a wave mask, as a 32-bit scalar (two s_bcnt1_i32_b32): compares against it stay on the SALU
+__device__ __forceinline__ uint32_t lanes32(unsigned long long m) {
+    return (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32));
+}
 #ifndef ARX_TRACE_IDXEN
 #define ARX_TRACE_IDXEN 1  // QNode2 loads indexed by node (idxen, a 32-B stride resource): no address VALU (C3 -1.6 %, profiles/r05/ab_idxen.txt); 0: byte offsets
 #endif
@@ -446,7 +450,7 @@ __device__ __forceinline__ uint4 node_half(__amdgpu_buffer_rsrc_t rs, int node, 
 //        origins on the grid, far below the 0.1-step outward margin of every quantized plane
 //        (quantize_nodes16; the launcher checks the emitter is on the grid).
 //   f32: the coded BvhNode (56 of its 64 B), ix = inv, oix = o*inv.
-template <int FMT, typename Stack>
+template <int FMT, typename Stack, bool PIN = true>
 __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
                                           __amdgpu_buffer_rsrc_t rs, const uint4* __restrict__ ncache) {
     constexpr bool Q16 = FMT == kFmtQ16;
@@ -544,7 +548,9 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     const int c_near = near1 ? c1 : c0;
     const int c_far = near1 ? c0 : c1;
     stk.put(sp, c_far);  // above the top of the stack unless pushed
-    asm volatile("" : "+v"(top));            // the pop read stays unconditional (no branch around it)
+    // PIN: an empty asm keeps the pop read unconditional (no branch around it); the small-launch
+    // instance leaves it to the compiler, which keeps it unconditional too, without the asm's s_nop
+    if constexpr (PIN) asm volatile("" : "+v"(top));
     const bool any = h0 | h1, both = h0 & h1;
     if constexpr (Stack::kSentinel) {  // row 0 holds -1: a pop of the empty stack ends the query
         // near1 -> c1; else h0 -> c0; else neither child was hit (near1 is false only with !h1 or h0)
@@ -740,7 +746,10 @@ constexpr int kDynShare = ARX_TRACE_DYN_SHARE, kDynChunk = ARX_TRACE_DYN_CHUNK, 
 // loop: NSTEPS guarded node steps per iteration; leaves are postponed and intersected wave-wide
 // once LEAF_THRESH lanes hold one (or no lane can step); the loop is left when THRESH lanes wait
 // for shading.
-template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT, bool GSTACK>
+// LEAN (the small-launch instance): no per-lane "traversing" flag -- a lane's query is done when its
+// node is -1 -- so the inner loop counts the lanes waiting for shading from wave masks on the SALU
+// (C2 0.366 -> 0.350 ms; the pool instance measured +1 % with it, profiles/r05/ab_loop.txt).
+template <int BLOCK, int THRESH, int LEAF_THRESH, int MINW, int NSTEPS, int FMT, bool GSTACK, bool LEAN = false>
 __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     constexpr bool Q16 = FMT == kFmtQ16;
     constexpr bool W4 = FMT == kFmtW4;
@@ -821,14 +830,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
 #if ARX_TRACE_PROF
         ++pf[10];
         {
-            const unsigned long long sh = __ballot(active && !trav);
+            const unsigned long long sh = __ballot(active && (LEAN ? t.node == -1 : !trav));
             if (sh) {
                 ++pf[8];
                 pf[9] += __popcll(sh);
             }
         }
 #endif
-        if (active && !trav) {
+        if (active && (LEAN ? t.node == -1 : !trav)) {  // the query is done: shade it
             shade(a, tbase, s, r, t.best, n_rx, n_miss);
             if (!wants_query(a, s)) active = false;
         }
@@ -864,7 +873,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             }
             if (w_next >= w_end && n_dyn == 0) exhausted = true;
         }
-        if (active && !trav) {
+        if (active && (LEAN ? t.node == -1 : !trav)) {
             ++n_q;
             setup_ray(r, s.pos, s.dir);
             if constexpr (Q16 || W4) {  // grid form of the slab planes (node_step, node_step_w4)
@@ -897,16 +906,21 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             if (exhausted) break;
             continue;
         }
+        const unsigned long long m_active = LEAN ? __ballot(active) : 0ull;  // fixed inside the traversal loop
         while (true) {
-            if (trav && t.node == -1) trav = false;  // query done (its stack is empty)
+            if (!LEAN && trav && t.node == -1) trav = false;  // query done (its stack is empty)
             const unsigned long long m_node = __ballot(t.node >= 0);
             const unsigned long long m_leaf = __ballot(t.node <= -2);
             if ((m_node | m_leaf) == 0ull) break;
-            if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            if constexpr (LEAN) {  // active lanes whose query is done (node -1) wait to be shaded
+                if (lanes32(m_active & ~(m_node | m_leaf)) >= (uint32_t)THRESH) break;
+            } else {
+                if (__popcll(__ballot(active && !trav)) >= THRESH) break;
+            }
 #if ARX_TRACE_PROF
             ++pf[11];
 #endif
-            if (m_node != 0ull && __popcll(m_leaf) < LEAF_THRESH) {
+            if (m_node != 0ull && (LEAN ? lanes32(m_leaf) < (uint32_t)LEAF_THRESH : __popcll(m_leaf) < LEAF_THRESH)) {
 #pragma unroll
                 for (int k = 0; k < NSTEPS; ++k) {
 #if ARX_TRACE_PROF
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                         ++n_steps;
 #endif
                         if constexpr (W4) node_step_w4(r, oix, oiy, oiz, t, stk, nrs);
-                        else node_step<FMT>(r, oix, oiy, oiz, t, stk, nrs, ncache);
+                        else node_step<FMT, Stack, !LEAN>(r, oix, oiy, oiz, t, stk, nrs, ncache);
                     }
                 }
             } else {
@@ -1077,7 +1091,7 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2
         constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
         const int g2 = trace_grid<SB, GSTACK, FMT>(args, cus, n_rays);
-        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK>), dim3(g2), dim3(SB),
+        hipLaunchKernelGGL((trace_kernel<SB, kThresh, kSmallLeaf, kWaves, kSmallSteps, FMT, GSTACK, true>), dim3(g2), dim3(SB),
                            dyn_lds, s, a2);
     } else {
         hipLaunchKernelGGL((trace_kernel<kBlock, kThresh, kLeafThresh, kWaves, kSteps, FMT, GSTACK>), dim3(grid),
@@ -1116,19 +1130,19 @@ bool trace_uses_small_block(const TraceArgs& a, int cus, bool force_global_stack
 }
 
 namespace {
-template <int B, int L, int S>
+template <int B, int L, int S, bool LEAN>
 const void* lds_stack_instance(int fmt) {
-    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtW4, false>)
-           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtQ16, false>)
-                            : reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtF32, false>);
+    return fmt == kFmtW4    ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtW4, false, LEAN>)
+           : fmt == kFmtQ16 ? reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtQ16, false, LEAN>)
+                            : reinterpret_cast<const void*>(trace_kernel<B, kThresh, L, kWaves, S, kFmtF32, false, LEAN>);
 }
 }  // namespace
 
 hipError_t trace_kernel_occupancy(int fmt, bool small, int* vgprs, int* waves_admitted, int* waves_target) {
     hipFuncAttributes fa;
     constexpr int SB = kSmallBlock > 0 ? kSmallBlock : kBlock;
-    const void* k = small ? lds_stack_instance<SB, kSmallLeaf, kSmallSteps>(fmt)
-                          : lds_stack_instance<kBlock, kLeafThresh, kSteps>(fmt);
+    const void* k = small ? lds_stack_instance<SB, kSmallLeaf, kSmallSteps, true>(fmt)
+                          : lds_stack_instance<kBlock, kLeafThresh, kSteps, false>(fmt);
     const hipError_t e = hipFuncGetAttributes(&fa, k);
     if (e != hipSuccess) return e;
     // gfx950: 512 VGPRs per SIMD lane slot, allocated in granules of 8

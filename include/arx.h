@@ -252,10 +252,14 @@ arx_status arx_group_set_mono_output(arx_group* g, int mono);
 arx_status arx_group_set_seed(arx_group* g, uint64_t seed);
 /* render() over the group: clear, trace every local shard, all-reduce, finalize on every member
  * (async on the members' streams).  render_ms (if not NULL; synchronises) = the longest shard's
- * trace kernel time. */
+ * trace kernel time.  After an error the members may be at different frames (and, on the rank path,
+ * peers may wait in the collective this rank skipped): destroy the group, do not render on it again. */
 arx_status arx_group_render(arx_group* g, double* render_ms);
 /* arx_set_frames_in_flight on every member; a member's all-reduce waits for its previous one, so
- * the collectives on each communicator keep their order. */
+ * the collectives on each communicator keep their order.  That event chain runs on one GPU with
+ * every collective forced (arx_debug_group_force_collectives, tests/test_gpu_collectives.py: 1 to 3
+ * frames, in and out of place, bit-identical to a plain renderer); its first multi-GPU run is the
+ * 8-GPU bench, which keeps the one-GPU frames-in-flight policy at every N. */
 arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n);
 arx_status arx_group_synchronize(arx_group* g);
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
