@@ -562,54 +562,6 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     }
 }
 
-#ifndef ARX_TRACE_LEANPF
-#define ARX_TRACE_LEANPF 0  // 1: the small-launch instance's node step prefetches both children's nodes
-#endif
-// The small-launch node step with child prefetch (ARX_TRACE_LEANPF): a launch of about one ray per
-// lane takes as long as its slowest wave's chain of dependent steps (fetch -> planes -> next node),
-// and the GPU has load slots to spare.  As soon as a node's data is in registers its two children's
-// nodes are fetched (a leaf or empty child's negative code indexes past the buffer: zeros, no access),
-// so a step that descends -- 85 % of them (bvh_stats: 15 % of visits hit no child) -- finds its data
-// already fetched while the planes were computed; only a pop waits for a fresh fetch.
-struct NodePf {
-    uint4 A, B;  // the current node's two halves, when `have`
-    bool have;
-};
-template <typename Stack>
-__device__ __forceinline__ void node_step_pf(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
-                                             __amdgpu_buffer_rsrc_t rs, NodePf& pf) {
-    const int sp = t.sp;
-    int top = stk.below(sp);
-    if (!pf.have) {
-        pf.A = node_half(rs, t.node, 0);
-        pf.B = node_half(rs, t.node, 1);
-    }
-    const uint4 A = pf.A, B = pf.B;
-    const int c0 = (int)A.w, c1 = (int)B.w;
-    const uint4 P0 = node_half(rs, c0, 0), Q0 = node_half(rs, c0, 1);
-    const uint4 P1 = node_half(rs, c1, 0), Q1 = node_half(rs, c1, 1);
-    const float ix = r.inv[0], iy = r.inv[1], iz = r.inv[2];
-    auto pl = [](uint32_t w, uint32_t sel) { return __uint_as_float(__builtin_amdgcn_perm(w, 0x4B000000u, sel)); };
-    const float nx0 = __builtin_fmaf(pl(A.x, r.nsel[0]), ix, -oix), fx0 = __builtin_fmaf(pl(A.x, r.fsel[0]), ix, -oix);
-    const float ny0 = __builtin_fmaf(pl(A.y, r.nsel[1]), iy, -oiy), fy0 = __builtin_fmaf(pl(A.y, r.fsel[1]), iy, -oiy);
-    const float nz0 = __builtin_fmaf(pl(A.z, r.nsel[2]), iz, -oiz), fz0 = __builtin_fmaf(pl(A.z, r.fsel[2]), iz, -oiz);
-    const float nx1 = __builtin_fmaf(pl(B.x, r.nsel[0]), ix, -oix), fx1 = __builtin_fmaf(pl(B.x, r.fsel[0]), ix, -oix);
-    const float ny1 = __builtin_fmaf(pl(B.y, r.nsel[1]), iy, -oiy), fy1 = __builtin_fmaf(pl(B.y, r.fsel[1]), iy, -oiy);
-    const float nz1 = __builtin_fmaf(pl(B.z, r.nsel[2]), iz, -oiz), fz1 = __builtin_fmaf(pl(B.z, r.fsel[2]), iz, -oiz);
-    const float tn0 = fmaxf(fmaxf(fmaxf(nx0, ny0), nz0), 0.0f);
-    const float tf0 = fminf(fminf(fminf(fx0, fy0), fz0), t.best.t);
-    const float tn1 = fmaxf(fmaxf(fmaxf(nx1, ny1), nz1), 0.0f);
-    const float tf1 = fminf(fminf(fminf(fx1, fy1), fz1), t.best.t);
-    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
-    const bool near1 = h1 & (!h0 | (tn1 < tn0));
-    stk.put(sp, near1 ? c0 : c1);  // the far child, above the top of the stack unless pushed
-    t.node = near1 ? c1 : (h0 ? c0 : top);
-    t.sp = sp + (h0 ? 0 : -1) + (int)h1;
-    pf.A = near1 ? P1 : P0;
-    pf.B = near1 ? Q1 : Q0;
-    pf.have = (h0 | h1) & (t.node >= 0);  // descended into an inner child: its data is fetched
-}
-
 // CW4 step (arx_layout.hpp): one 32-B node = two 16-B loads for four children.  Plane q of axis k
 // is 4*o_k + q*2^e_k grid quanta, so t = fma(q, ix*2^e, fma(o, 4*ix, -oix)) (ix*2^e exact): the
 // Q16 slab arithmetic with the frame folded in.  The hit children are sorted by entry distance
@@ -874,9 +826,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     t.node = -1;
     t.sp = 0;
     float oix = 0.f, oiy = 0.f, oiz = 0.f;
-    constexpr bool PF = LEAN && Q16 && !GSTACK && ARX_TRACE_LEANPF && ARX_TRACE_BITFLOAT && ARX_TRACE_SIGNSEL;
-    NodePf pf;
-    pf.have = false;
     while (true) {
 #if ARX_TRACE_PROF
         ++pf[10];
@@ -952,7 +901,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             t.node = 0;  // the top node (node 0; unit 0 of the CW4 buffer)
             t.sp = 0;
             trav = true;
-            if constexpr (PF) pf.have = false;
         }
         if (__ballot(active) == 0ull) {
             if (exhausted) break;
@@ -987,7 +935,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                         ++n_steps;
 #endif
                         if constexpr (W4) node_step_w4(r, oix, oiy, oiz, t, stk, nrs);
-                        else if constexpr (PF) node_step_pf(r, oix, oiy, oiz, t, stk, nrs, pf);
                         else node_step<FMT, Stack, !LEAN>(r, oix, oiy, oiz, t, stk, nrs, ncache);
                     }
                 }
@@ -999,13 +946,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
 #if ARX_TRACE_COUNT
                 if (t.node <= -2) n_tris += (uint32_t)((~t.node) & (W4 ? 3 : 15));
 #endif
-                if constexpr (PF) {
-                    const bool was_leaf = t.node <= -2;
-                    leaf_step<FMT>(trs, r, t, stk);
-                    if (was_leaf) pf.have = false;  // a leaf's lane continues from a pop
-                } else {
-                    leaf_step<FMT>(trs, r, t, stk);
-                }
+                leaf_step<FMT>(trs, r, t, stk);
             }
         }
     }
@@ -1106,9 +1047,8 @@ constexpr int kSmallBlock = ARX_TRACE_SMALL_BLOCK;
 #define ARX_TRACE_SMALL_LEAF 8
 #endif
 constexpr int kSmallSteps = ARX_TRACE_SMALL_STEPS, kSmallLeaf = ARX_TRACE_SMALL_LEAF;
-// waves per SIMD the small-launch instance is compiled for (its launches fill 1.5 - 2 per SIMD; the
-// prefetching step needs the registers of two more nodes)
-constexpr int kSmallWaves = ARX_TRACE_LEANPF ? 4 : ARX_TRACE_WAVES;
+// waves per SIMD the small-launch instance is compiled for
+constexpr int kSmallWaves = ARX_TRACE_WAVES;
 constexpr int kThresh = ARX_TRACE_THRESH, kLeafThresh = ARX_TRACE_LEAF_THRESH, kWaves = ARX_TRACE_WAVES, kSteps = ARX_TRACE_STEPS;
 constexpr int kSimdsPerCu = 4;
 

@@ -71,7 +71,8 @@ def bytes_per_bounce(n_tris: int) -> int:
 
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
 NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2", 2: "4-wide compressed (CW4)"}  # arx_stats.trace_format
-PROFILES = "r04"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
+PROFILES = "r05"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
+CONV_TRAFFIC = "r04/conv_traffic_r04j.json"  # the full convolution's PMC traffic (its kernels are unchanged since)
 
 
 # ----------------------------------------------------------------------------- rank plumbing ---
@@ -603,7 +604,7 @@ def main(argv=None) -> int:
                                        ("workload", "tree_hash", "trace_kernel_id"))
     td, td_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_td_c3.json")), args.workload, st0)
     vmem, vmem_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_vmem_ceiling.json")), args.workload, st0)
-    conv_traffic = load_profile(os.path.join(PROFILES, "conv_traffic_r04j.json"))
+    conv_traffic = load_profile(CONV_TRAFFIC)
     conv_frames_s = world * frames / (conv_ms_max * 1e-3)  # the convolution kernels' own window
     conv_frames_step = world * frames * args.steps / elapsed  # the pipeline: frames convolved per timed step
     result = {
@@ -695,7 +696,7 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
             "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and args.workload == "c3" else None,
             "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and args.workload == "c3" else None,
-            "traffic_source": f"profiles/{PROFILES}/conv_traffic_r04j.json (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
+            "traffic_source": f"profiles/{CONV_TRAFFIC} (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
                               "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
         },
     }
