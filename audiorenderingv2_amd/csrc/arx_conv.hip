@@ -742,23 +742,14 @@ constexpr int ct_ns(int L, int s) {
     return ns;
 }
 
-// LW: lanes per FFT -- 64 (one wave, wave barriers) or 128 (two waves of the block, block barriers:
-// every wave of the block runs the same stages)
-template <int LW>
-__device__ __forceinline__ void fft_barrier() {
-    if constexpr (LW == 64)
-        __builtin_amdgcn_wave_barrier();
-    else
-        __syncthreads();
-}
-template <int R, int NS, int L, bool SWI, bool SWO, int LW = 64>
+template <int R, int NS, int L, bool SWI, bool SWO>
 __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, int j, int sign) {
-    constexpr int nb = L / R, step = L / (NS * R), kB = (nb + LW - 1) / LW;
+    constexpr int nb = L / R, step = L / (NS * R), kB = (nb + 63) / 64;
     double2 v[kB][R];
 #pragma unroll
     for (int i = 0; i < kB; ++i) {
-        const int b = j + LW * i;
-        if (nb % LW == 0 || i < kB - 1 || b < nb) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
             const int k = b % NS;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
@@ -772,26 +763,26 @@ __device__ __forceinline__ void mr_stage_ct(double2* buf, const double2* twl, in
             dft_radix<R>(v[i], sign);
         }
     }
-    fft_barrier<LW>();
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < kB; ++i) {
-        const int b = j + LW * i;
-        if (nb % LW == 0 || i < kB - 1 || b < nb) {
+        const int b = j + 64 * i;
+        if (nb % 64 == 0 || i < kB - 1 || b < nb) {
             const int k = b % NS;
             const int d = (b - k) * R + k;
 #pragma unroll
             for (int q = 0; q < R; ++q) buf[lds_ix<SWO>(d + q * NS, L & ~7)] = v[i][q];
         }
     }
-    fft_barrier<LW>();
+    __builtin_amdgcn_wave_barrier();
 }
 
-template <int L, int S, int LW = 64>
+template <int L, int S>
 __device__ __forceinline__ void fft_ct_stages(double2* buf, const double2* twl, int j, int sign) {
     if constexpr (ct_radix(L, S) != 0) {
         constexpr bool sw = L % 2 == 0;  // swizzled between the first two stages (lds_ix)
-        mr_stage_ct<ct_radix(L, S), ct_ns(L, S), L, sw && S == 1, sw && S == 0, LW>(buf, twl, j, sign);
-        fft_ct_stages<L, S + 1, LW>(buf, twl, j, sign);
+        mr_stage_ct<ct_radix(L, S), ct_ns(L, S), L, sw && S == 1, sw && S == 0>(buf, twl, j, sign);
+        fft_ct_stages<L, S + 1>(buf, twl, j, sign);
     }
 }
 
@@ -863,25 +854,13 @@ __device__ __forceinline__ void fft2_wave_any(double2* buf0, double2* buf1, cons
 
 // In-place FFT of one row / column by one wave: the compile-time plan when L > 0, else the
 // run-time plan f (R7 / LM: see fft_mr_wave).
-template <bool R7, int LM, int L, int LW = 64>
+template <bool R7, int LM, int L>
 __device__ __forceinline__ void fft_wave_any(double2* buf, const double2* twl, const Factors& f, int j, int sign) {
-    static_assert(LW == 64 || L > 0, "two waves per FFT only for the compile-time plans");
     if constexpr (L > 0)
-        fft_ct_stages<L, 0, LW>(buf, twl, j, sign);
+        fft_ct_stages<L, 0>(buf, twl, j, sign);
     else
         fft_mr_wave<R7, LM>(buf, twl, f, j, sign);
 }
-
-// Lanes per column FFT in passes A and C: two waves for the compile-time plans (ARX_CONV_WIDE), so
-// stages of 65 .. 128 butterflies (300 = 4 3 5 5: 75, 100, 60, 60) take one round instead of two.
-#ifndef ARX_CONV_WIDE
-#define ARX_CONV_WIDE 0
-#endif
-template <int L>
-constexpr int col_lanes() { return (ARX_CONV_WIDE && L > 0) ? 128 : 64; }
-// columns per block of passes A / C for blocks of `waves` waves
-template <int L>
-constexpr int cols_per_block(int waves) { return waves * 64 / col_lanes<L>(); }
 
 // Workgroups are dealt round-robin over the 8 XCDs: give each XCD a contiguous run of tiles, so
 // that the tiles sharing a 128-B line (pass A's f32 rows, pass C's f64 rows) share its L2.
@@ -970,8 +949,7 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     constexpr int IT = LM / 64;  // per-lane elements of a column, per-thread tile loads
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
-    constexpr int CW = col_lanes<L1>();
-    const int nt = blockDim.x, tc = nt / CW, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
+    const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2;
     const int64_t batch = blockIdx.y;
     const bool ir = MODE == 1 || (MODE == 0 && batch >= a.n_pairs);
     const int64_t ch = MODE == 1 ? batch : batch - a.n_pairs;
@@ -1015,7 +993,7 @@ __global__ __launch_bounds__(512) void pass_a_mr(MrArgs m) {
     }
     __syncthreads();
     CONV_PROF_MARK(1);
-    fft_wave_any<R7, LM, L1, CW>(lds + (size_t)(threadIdx.x / CW) * sc, twl, m.f1, threadIdx.x % CW, -1);
+    fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, -1);
     __syncthreads();
     CONV_PROF_MARK(2);
     double2* dst = MODE == 0 && ir ? a.G : ir ? a.H + (size_t)ch * a.M : a.S + (size_t)batch * 3 * a.M;
@@ -1324,8 +1302,7 @@ __device__ __forceinline__ void pass_c_chain_body(const MrArgs& m) {
     constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
     const PassArgs& a = m.p;
-    constexpr int CW = col_lanes<L1>();
-    const int nt = blockDim.x, tc = nt / CW, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2, half = N1 >> 1;
+    const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2, half = N1 >> 1;
     const int ch = blockIdx.y & 1;
     const int64_t p0 = (int64_t)(blockIdx.y >> 1) * m.chain;
     const int64_t p1 = p0 + m.chain < a.n_pairs ? p0 + m.chain : a.n_pairs;
@@ -1363,7 +1340,7 @@ __device__ __forceinline__ void pass_c_chain_body(const MrArgs& m) {
         if (pair == pstart) CONV_PROF_MARK(1);
 #endif
         if (pair + 1 < p1) load(pair + 1);  // in flight during this pair's FFT
-        fft_wave_any<R7, LM, L1, CW>(lds + (size_t)(threadIdx.x / CW) * sc, twl, m.f1, threadIdx.x % CW, +1);
+        fft_wave_any<R7, LM, L1>(lds + (size_t)(threadIdx.x >> 6) * sc, twl, m.f1, threadIdx.x & 63, +1);
         __syncthreads();
 #if ARX_CONV_PROF
         if (pair == pstart) CONV_PROF_MARK(2);
@@ -1615,8 +1592,7 @@ static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipS
 template <bool R7, int LM, int L1, int L2>
 static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     const MrArgs m = mr_args(p, a);
-    constexpr int c2 = cols_per_block<L1>(2);
-    hipLaunchKernelGGL((pass_a_mr<1, R7, LM, L1>), dim3(mr_tiles(p, c2), 2), dim3(128), mr_lds_a(p, c2), s, m);
+    hipLaunchKernelGGL((pass_a_mr<1, R7, LM, L1>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
     launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
 }
 
@@ -1641,9 +1617,8 @@ static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipSt
 template <bool R7, int LM, int L1, int L2>
 static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool with_ir, hipStream_t s) {
     MrArgs m = mr_args(p, a);
-    constexpr int ca = cols_per_block<L1>(ARX_CONV_TCA);
-    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ca), (unsigned)(pairs + (with_ir ? 1 : 0))),
-                       dim3(64 * ARX_CONV_TCA), mr_lds_a(p, ca), s, m);
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)(pairs + (with_ir ? 1 : 0))),
+                       dim3(64 * ARX_CONV_TCA), mr_lds_a(p, ARX_CONV_TCA), s, m);
     if (with_ir)
         launch_b_pair<R7, LM, L2>(p, (int)pairs, m, s);
     else
@@ -1656,9 +1631,8 @@ static void mr_file(const ConvPlan* p, const PassArgs& a, int64_t pairs, bool wi
 template <bool R7, int LM, int L1, int L2>
 static void mr_prepare(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipStream_t s) {
     MrArgs m = mr_args(p, a);
-    constexpr int ca = cols_per_block<L1>(ARX_CONV_TCA);
-    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ca), (unsigned)pairs), dim3(64 * ARX_CONV_TCA),
-                       mr_lds_a(p, ca), s, m);
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), (unsigned)pairs), dim3(64 * ARX_CONV_TCA),
+                       mr_lds_a(p, ARX_CONV_TCA), s, m);
     launch_b_mr<3, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
 }
 
@@ -1670,9 +1644,8 @@ static void mr_prepared(const ConvPlan* p, const PassArgs& a, int64_t pairs, boo
     if (with_ir) {
         MrArgs mi = m;
         mi.p.n_pairs = 0;  // batch 0 of this launch is the IR (pass_a_mr mode 0's batch past the pairs)
-        constexpr int ca = cols_per_block<L1>(ARX_CONV_TCA);
-        hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ca), 1u), dim3(64 * ARX_CONV_TCA),
-                           mr_lds_a(p, ca), s, mi);
+        hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), 1u), dim3(64 * ARX_CONV_TCA),
+                           mr_lds_a(p, ARX_CONV_TCA), s, mi);
         launch_b_pair<R7, LM, L2, true>(p, (int)pairs, m, s);
     } else {
         launch_b_mr<4, R7, LM, L2>(p, ARX_CONV_ROWSB, (int)pairs, m, s);
@@ -1687,11 +1660,11 @@ static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipSt
         m.chain = ARX_CONV_CHAIN;
         const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
         if constexpr (L1 > 0)
-            hipLaunchKernelGGL((pass_c_chain3<R7, LM, L1>), dim3(mr_tiles(p, cols_per_block<L1>(ARX_CONV_TCC)), 2 * chains),
-                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, cols_per_block<L1>(ARX_CONV_TCC)), s, m);
+            hipLaunchKernelGGL((pass_c_chain3<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains),
+                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
         else
-            hipLaunchKernelGGL((pass_c_chain<R7, LM, L1>), dim3(mr_tiles(p, cols_per_block<L1>(ARX_CONV_TCC)), 2 * chains),
-                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, cols_per_block<L1>(ARX_CONV_TCC)), s, m);
+            hipLaunchKernelGGL((pass_c_chain<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains),
+                               dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
         return;
     }
     hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), (unsigned)(2 * pairs)),
@@ -1702,8 +1675,7 @@ static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipSt
 template <bool R7, int LM, int L1, int L2>
 static void mr_live(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     const MrArgs m = mr_args(p, a);
-    constexpr int c2 = cols_per_block<L1>(2);
-    hipLaunchKernelGGL((pass_a_mr<2, R7, LM, L1>), dim3(mr_tiles(p, c2), 1), dim3(128), mr_lds_a(p, c2), s, m);
+    hipLaunchKernelGGL((pass_a_mr<2, R7, LM, L1>), dim3(mr_tiles(p, 2), 1), dim3(128), mr_lds_a(p, 2), s, m);
     launch_b_mr<0, R7, LM, L2>(p, 1, 1, m, s);
     hipLaunchKernelGGL((pass_c_mr<R7, LM, L1>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_c(p, 2), s, m);
 }
