@@ -141,9 +141,10 @@ class Ranks:
     """Barrier / max / sum over the job's processes: RCCL all-reduces of the group itself (one
     process driving every GPU needs none)."""
 
-    def __init__(self, group, mode: str):
+    def __init__(self, group, mode: str, forced: bool = False):
         self.g = group
-        self.multi = mode == "rank" and group.n_ranks > 1
+        # forced (--debug-force-collectives): the one-rank group issues them too (tests only)
+        self.multi = (mode == "rank" and group.n_ranks > 1) or forced
 
     def barrier(self) -> None:
         if self.multi:
@@ -413,6 +414,10 @@ def main(argv=None) -> int:
                          "that chain with every collective forced on one GPU)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
+    ap.add_argument("--debug-force-collectives", action="store_true",
+                    help="tests only: every group collective is issued even at one rank (the histogram all-reduce "
+                         "with frames in flight, the barriers and max-over-ranks, the rank path's scene broadcast), "
+                         "so a one-GPU box runs the multi-GPU job's collective path (arx_debug_group_force_collectives)")
     ap.add_argument("--process-group", action="store_true",
                     help="take the one-GPU-per-process (RCCL rank) path even at one rank: a rehearsal of the "
                          "torch.distributed.run path on a one-GPU box")
@@ -453,11 +458,15 @@ def main(argv=None) -> int:
     with _stdout_to_stderr():  # RCCL prints its version banner on stdout; stdout is the JSON line only
         if plan["mode"] == "rank":
             uids = share_unique_ids(rank, world, os.environ, RenderGroup.unique_id, 3)
-            g = RenderGroup.rank(settings, world, rank, uids[0], scene=scene, receiver=receiver)
+            g = RenderGroup.rank(settings, world, rank, uids[0])
         else:
             uids = [None, None, None]
-            g = RenderGroup(settings, devices=plan["devices"], scene=scene, receiver=receiver)
-    ranks = Ranks(g, plan["mode"])
+            g = RenderGroup(settings, devices=plan["devices"])
+        if args.debug_force_collectives:
+            g.debug_force_collectives(True, True)
+        g.set_receiver_model(*receiver)
+        g.set_scene(scene)  # the rank path: rank 0 builds, the tree reaches the other ranks over RCCL
+    ranks = Ranks(g, plan["mode"], args.debug_force_collectives)
     ranks.barrier()
     if plan["mode"] == "rank" and rank == 0 and world > 1:
         with contextlib.suppress(OSError):
@@ -512,6 +521,7 @@ def main(argv=None) -> int:
     t1 = time.perf_counter()
     elapsed = ranks.max(t1 - t0)
     stats = g.stats()
+    collectives = g.debug_collectives()  # the headline group's, up to the end of the timed steps
     q_proc = int(stats["queries"])  # this process's members, per step (counters cleared every step)
     q_all = int(round(ranks.sum(q_proc)))
     m0 = members[0]
@@ -591,9 +601,13 @@ def main(argv=None) -> int:
                             max_bounces=C5["max_bounces"], hrtf_absorption_rate=1.0, seed=1, device=plan["devices"][0])
         with _stdout_to_stderr():
             if plan["mode"] == "rank":
-                g5 = RenderGroup.rank(s5, world, rank, uids[2], scene=scene, receiver=receiver)
+                g5 = RenderGroup.rank(s5, world, rank, uids[2])
             else:
-                g5 = RenderGroup(s5, devices=plan["devices"], scene=scene, receiver=receiver)
+                g5 = RenderGroup(s5, devices=plan["devices"])
+            if args.debug_force_collectives:
+                g5.debug_force_collectives(True, True)
+            g5.set_receiver_model(*receiver)
+            g5.set_scene(scene)
         g5.setEmitterPosInOptix(CONFERENCE_EMITTER)
         moving = moving_listener(g5, ranks, args.c5_frames, int(np.prod(C5["rays"])) // world)
         g5.close()
@@ -640,6 +654,9 @@ def main(argv=None) -> int:
                             + ")"),
         },
         "runtime": runtime_info(),
+        "collectives_issued": dict(collectives, forced=bool(args.debug_force_collectives),
+                                   note="RCCL collectives the headline group issued up to the end of the timed steps "
+                                        "(a one-rank group skips them unless forced)"),
         "setup_s_rank0": setup_s,
         "single_frame": single_frame,
         "preroll": {"steps": pre_steps, "seconds_rank0": preroll_s,

@@ -126,3 +126,62 @@ def test_force_refused_without_a_communicator():
             g.debug_force_collectives(True)
     finally:
         g.close()
+
+
+# ---- one-GPU equivalents of tests/test_gpu_multi.py (which needs >= 2 GPUs) -------------------
+C4 = dict(rays=(1000, 100, 100), sample_rate=48000, base_power=3.62, max_bounces=32, hrtf_absorption_rate=0.5)
+
+
+@pytest.mark.parametrize("rank_path", [False, True])
+def test_forced_group_equals_one_renderer_c4(conference, rank_path):
+    """test_gpu_multi.py's C4 group test at one GPU: the forced group (ncclCommInitAll over [0], or a
+    one-rank ncclCommInitRank group; either way its scene comes through the broadcast) renders two
+    seeds back to back, frames in flight on, every all-reduce out of place; each IR bit-identical to
+    a renderer's."""
+    s = RenderSettings(**C4)
+    r = AudioRenderer(s, scene=conference, receiver=receiver_local())
+    g = RenderGroup.rank(s, 1, 0, RenderGroup.unique_id()) if rank_path else RenderGroup(s, devices=[0])
+    try:
+        g.debug_force_collectives(True, True)
+        g.set_receiver_model(*receiver_local())
+        g.set_scene(conference)
+        g.set_frames_in_flight(2)
+        for x in (g, r):
+            x.setEmitterPosInOptix(CONFERENCE_EMITTER)
+            x.setSphereCenterInOptix(CONFERENCE_LISTENER, 30.0)
+        for seed in (1, 2):
+            g.set_seed(seed)
+            r.set_seed(seed)
+            g.render()
+            r.render()
+            ref = r.get_ir()
+            assert ref[0].any()
+            got = g.member(0).get_ir()
+            assert np.array_equal(bits(got[0]), bits(ref[0])) and np.array_equal(bits(got[1]), bits(ref[1])), seed
+            gs, rs = g.stats(), r.stats()
+            assert (gs["queries"], gs["receiver_hits"], gs["misses"]) == (rs["queries"], rs["receiver_hits"],
+                                                                          rs["misses"])
+        n = g.debug_collectives()
+        # a forced one-member group takes the rank path's scene hand-over either way (arx_group_set_scene)
+        assert n["histogram_allreduce"] == 2 and n["scene_broadcast"] == 1
+    finally:
+        g.close()
+        r.close()
+
+
+def test_bench_forced_collectives_count_the_plain_launch():
+    """test_gpu_multi.py's bench test at one GPU: bench.py --debug-force-collectives as one
+    torch.distributed.run rank (ncclCommInitRank, the scene broadcast, barriers and max-over-ranks
+    over RCCL) and as one process (ncclCommInitAll) counts the plain line's ray-bounces per step."""
+    from test_gpu_multi import _bench
+    plain = _bench(["--gpus", "1"], timeout=240)
+    ranks = _bench(["--gpus", "1", "--process-group", "--debug-force-collectives"], torchrun_ranks=1, timeout=240)
+    local = _bench(["--gpus", "1", "--debug-force-collectives"], timeout=240)
+    assert "ncclCommInitRank" in ranks["config"]["parallelism"]
+    assert "ncclCommInitAll" in local["config"]["parallelism"]
+    assert ranks["ray_bounces_per_step"] == local["ray_bounces_per_step"] == plain["ray_bounces_per_step"]
+    assert plain["collectives_issued"]["histogram_allreduce"] == 0 and not plain["collectives_issued"]["forced"]
+    for d in (ranks, local):
+        c = d["collectives_issued"]
+        assert c["forced"] and c["histogram_allreduce"] >= d["steps"] + d["warmup"], c
+        assert c["f64_allreduce"] > 0 and c["scene_broadcast"] == 1, c

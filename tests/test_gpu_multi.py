@@ -2,7 +2,10 @@
 
 Skipped on a one-GPU box (every test checks `device_count() >= 2` first); there the same code runs
 as a one-GPU RCCL group, a one-rank ncclCommInitRank group and oversubscribed groups
-(tests/test_gpu_group.py), and its host side in real processes (tests/test_distributed_gloo.py).
+(tests/test_gpu_group.py), with every collective forced at one rank -- including both tests below at
+the same shapes (tests/test_gpu_collectives.py: test_forced_group_equals_one_renderer_c4,
+test_bench_forced_collectives_count_the_plain_launch) -- and its host side in real processes
+(tests/test_distributed_gloo.py).
 
   * RenderGroup(devices=range(n)) -- one process, ncclCommInitAll, one int64 ncclAllReduce of the
     histogram -- at configs[3]'s shape (C4: 10 M rays x 32 bounces, 48 kHz): the IR on every member is
