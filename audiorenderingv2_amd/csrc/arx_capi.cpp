@@ -1528,9 +1528,16 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
     if (n > 0 && (!h_in || !h_out_left || !h_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
     if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the staging buffers below
-    hipEvent_t p0, p1;
-    ARX_HIP(hipEventCreate(&p0));
-    ARX_HIP(hipEventCreate(&p1));
+    struct Events {  // destroyed on every return below
+        hipEvent_t e[2] = {nullptr, nullptr};
+        ~Events() {
+            for (hipEvent_t x : e)
+                if (x) hipEventDestroy(x);
+        }
+    } ev;
+    ARX_HIP(hipEventCreate(&ev.e[0]));
+    ARX_HIP(hipEventCreate(&ev.e[1]));
+    hipEvent_t p0 = ev.e[0], p1 = ev.e[1];
     ARX_HIP(hipEventRecord(p0, r->stream));
     if (n > r->conv_cap) {
         hipFree(r->d_conv_in);
@@ -1560,8 +1567,6 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
         ARX_HIP(hipEventElapsedTime(&ms, p0, p1));
         *proc_ms = ms;
     }
-    hipEventDestroy(p0);
-    hipEventDestroy(p1);
     return ARX_OK;
 }
 

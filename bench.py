@@ -414,6 +414,9 @@ def main(argv=None) -> int:
                          "that chain with every collective forced on one GPU)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
+    ap.add_argument("--no-host-leg", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) leg: render + arx_convolute_audio_file from and to "
+                         "host memory")
     ap.add_argument("--debug-force-collectives", action="store_true",
                     help="tests only: every group collective is issued even at one rank (the histogram all-reduce "
                          "with frames in flight, the barriers and max-over-ranks, the rank path's scene broadcast), "
@@ -593,6 +596,38 @@ def main(argv=None) -> int:
                         "(arx_convolute_prepared) = the new IR's spectra + products + inverse transforms, "
                         "bit-identical to the full one (tests/test_gpu_conv_reuse.py); not the headline's work"}
         g.set_frames_in_flight(args.frames_in_flight)
+    # Host buffers (the PCIe-inclusive rate, never the value): the reference's full_render_cycle
+    # shape through the C ABI's host-memory entry point -- render, then arx_convolute_audio_file with
+    # the audio in host memory and both output channels back in host memory (AudioRenderer.cpp:663-750).
+    host_leg = None
+    if not args.no_host_leg:
+        g.set_frames_in_flight(1)
+
+        def step_host():
+            g.render(timed=False)
+            return [m.convoluteAudioFile(audio_np)[3] for m in members]
+
+        for _ in range(args.warmup):
+            step_host()
+        g.synchronize()
+        ranks.barrier()
+        t0h = time.perf_counter()
+        host_conv = []
+        for _ in range(args.steps):
+            host_conv.append(max(step_host()))
+        g.synchronize()
+        ranks.barrier()
+        elh = ranks.max(time.perf_counter() - t0h)
+        host_leg = {"ms_per_step": elh / args.steps * 1e3,
+                    "ray_bounces_per_s": q_all * args.steps / elh,
+                    "host_path_ms": float(ranks.max(np.median(host_conv))),
+                    "host_bytes_per_gpu_per_step": 3 * 4 * frames,
+                    "why": "the PCIe-inclusive rate, not the value: each step renders and then convolves the file "
+                           "from host memory into host memory (arx_convolute_audio_file: f32 samples in, both "
+                           "channels out), one frame in flight; host_path_ms = that call's median window on the renderer's stream "
+                           "(HIP events: host-to-device copy, IR spectra + convolution, both device-to-host copies), "
+                           "slowest GPU"}
+        g.set_frames_in_flight(args.frames_in_flight)
 
     n_tris = int(stats["n_scene_tris"] + stats["n_receiver_tris"])
     moving = None
@@ -675,6 +710,7 @@ def main(argv=None) -> int:
                                                     "window alone (the renderer's HIP events, arx_conv_times)"},
         "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms},
         "convolution_input_reuse": reuse,
+        "host_buffers": host_leg,
         "trace_kernel_build": {"vgprs": int(st0["trace_vgprs"]), "waves_per_simd": int(st0["trace_waves_per_simd"]),
                                "waves_target": int(st0["trace_waves_target"]),
                                "node_format": NODE_FORMATS.get(int(st0["trace_format"]), str(st0["trace_format"])),

@@ -69,6 +69,13 @@ def test_bench_prints_one_contract_line():
     sf = d["single_frame"]
     assert sf["value"] > 0 and sf["ms_per_step"] > 0
     assert d["phases_ms_rank0"]["trace_kernel"] < sf["ms_per_step"]
+    # the host-buffer (PCIe-inclusive) leg: never the value, its own rate beside it
+    hb = d["host_buffers"]
+    assert hb["ms_per_step"] > hb["host_path_ms"] > d["phases_ms_rank0"]["ir_spectra_and_convolution"]
+    assert abs(hb["ray_bounces_per_s"] - d["ray_bounces_per_step"] / (hb["ms_per_step"] * 1e-3)) < 1e-6 * hb["ray_bounces_per_s"]
+    assert hb["host_bytes_per_gpu_per_step"] == 12 * frames
+    # no collectives at one rank unless forced (tests/test_gpu_collectives.py forces them)
+    assert d["collectives_issued"]["histogram_allreduce"] == 0 and not d["collectives_issued"]["forced"]
 
 
 def test_bench_refuses_more_gpus_than_the_box_has():
