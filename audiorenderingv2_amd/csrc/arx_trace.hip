@@ -34,12 +34,6 @@
 #ifndef ARX_TRACE_SIGNSEL
 #define ARX_TRACE_SIGNSEL 1  // per-ray near/far plane selection in the 16-bit node step (0: min / max per slab)
 #endif
-#ifndef ARX_TRACE_DCULL
-#define ARX_TRACE_DCULL 0  // experiment: 7-bit entry-distance keys in the LDS stack words, pops culled after leaves
-#endif
-#ifndef ARX_TRACE_DCULL_KS
-#define ARX_TRACE_DCULL_KS 8.0f  // keys per metre
-#endif
 
 namespace arx {
 namespace {
@@ -389,18 +383,7 @@ struct Trav {
     Best best;  // closest hit so far
     int node;
     int sp;    // stack depth
-#if ARX_TRACE_DCULL
-    uint32_t bk;  // floor(best.t * KS) saturated at 127: a popped word whose key exceeds it is culled
-#endif
 };
-#if ARX_TRACE_DCULL
-// stack word = code << 7 | key: the child code (25 bits signed: leaf codes reach -(2^24) for a million
-// triangle records) over a 7-bit key floor(t_entry * KS) saturated at 127
-__device__ __forceinline__ int dcull_code(int w) { return w >> 7; }
-__device__ __forceinline__ uint32_t dcull_key(float t) {
-    return min((uint32_t)__builtin_amdgcn_cvt_pk_u8_f32(t * ARX_TRACE_DCULL_KS, 0u, 0u), 127u);
-}
-#endif
 
 // Traversal stack of one lane.  LDS: ROWS entries at stk[slot * BLOCK + lane].  Global (trees
 // deeper than the LDS rows): a column of bvh_depth + 1 entries at gstack[slot * lanes + gid],
@@ -564,18 +547,7 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
     const bool near1 = h1 & (!h0 | (tn1 < tn0));
     const int c_near = near1 ? c1 : c0;
     const int c_far = near1 ? c0 : c1;
-#if ARX_TRACE_DCULL
-    if constexpr (Stack::kSentinel && Q16) {
-        // the pushed word: the far child's code in bits 0..23, its entry distance's key in 24..31
-        const float t_far = near1 ? tn0 : tn1;
-        stk.put(sp, (int)(((uint32_t)c_far << 7) | dcull_key(t_far)));
-        top = dcull_code(top);
-    } else {
-        stk.put(sp, c_far);
-    }
-#else
     stk.put(sp, c_far);  // above the top of the stack unless pushed
-#endif
     // PIN: an empty asm keeps the pop read unconditional (no branch around it); the small-launch
     // instance leaves it to the compiler, which keeps it unconditional too, without the asm's s_nop
     if constexpr (PIN) asm volatile("" : "+v"(top));
@@ -718,35 +690,6 @@ __device__ __forceinline__ void leaf_step(__amdgpu_buffer_rsrc_t trs, const Ray&
     // made the compiler move the closest-hit state into other registers and back at every join).
     const bool more = count > 2;
     const int rest = FMT == kFmtW4 ? ~((unit + 6) * 4 + (count - 2)) : ~(((unit / 3) + 2) * 16 + (count - 2));
-#if ARX_TRACE_DCULL
-    if constexpr (Stack::kSentinel && FMT == kFmtQ16) {
-        // the closest hit may have moved nearer: entries whose key exceeds it are skipped (the two
-        // topmost checked; the sentinel row's key is 0)
-        t.bk = dcull_key(t.best.t);
-        const int sp = t.sp;
-#if ARX_TRACE_DCULL >= 2  // the four topmost entries: the first one not culled (the sentinel never is)
-        int w1 = stk.below(sp), w2 = stk.below(max(sp - 1, 0)), w3 = stk.below(max(sp - 2, 0)),
-            w4 = stk.below(max(sp - 3, 0));
-        asm volatile("" : "+v"(w1), "+v"(w2), "+v"(w3), "+v"(w4));
-        const bool c1 = ((uint32_t)w1 & 127u) > t.bk, c2 = ((uint32_t)w2 & 127u) > t.bk,
-                   c3 = ((uint32_t)w3 & 127u) > t.bk;
-        const bool pop = lf & !more;
-        const int top = dcull_code(!c1 ? w1 : (!c2 ? w2 : (!c3 ? w3 : w4)));
-        const int drop = !c1 ? 1 : (!c2 ? 2 : (!c3 ? 3 : 4));
-        t.node = lf ? (more ? rest : top) : t.node;
-        t.sp = pop ? sp - drop : sp;
-#else
-        int w1 = stk.below(sp), w2 = stk.below(max(sp - 1, 0));
-        asm volatile("" : "+v"(w1), "+v"(w2));
-        const bool c1 = ((uint32_t)w1 & 127u) > t.bk;
-        const bool pop = lf & !more;
-        const int top = dcull_code(c1 ? w2 : w1);
-        t.node = lf ? (more ? rest : top) : t.node;
-        t.sp = pop ? sp - 1 - (int)c1 : sp;
-#endif
-        return;
-    }
-#endif
     const int sp = t.sp;
     int top = stk.below(sp);
     asm volatile("" : "+v"(top));
@@ -837,11 +780,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
         stk.nrows = a.bvh_depth + 1;
     } else {
         stk.base = stk_lds + lane;
-#if ARX_TRACE_DCULL
-        stk_lds[lane] = Q16 ? (int)0xFFFFFF80u : -1;  // code -1 over a key of 0: never culled
-#else
         stk_lds[lane] = -1;  // the dummy row under the stack (LdsStack::kSentinel)
-#endif
     }
     const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf)
                                           : (Q16 ? buffer_rsrc(a.qnodes, ARX_TRACE_IDXEN ? (short)sizeof(QNode2) : (short)0)
@@ -961,9 +900,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
             t.best.unit = -1;
             t.node = 0;  // the top node (node 0; unit 0 of the CW4 buffer)
             t.sp = 0;
-#if ARX_TRACE_DCULL
-            t.bk = 127u;
-#endif
             trav = true;
         }
         if (__ballot(active) == 0ull) {
