@@ -98,3 +98,32 @@ def test_steps_beyond_the_timing_ring_are_refused():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "100000"], capture_output=True,
                        text=True, timeout=120)
     assert p.returncode != 0 and "--steps" in p.stderr and p.stdout.strip() == ""
+
+
+class _FakeGroup:
+    """A group stand-in that records the f64 all-reduces bench.Ranks issues."""
+
+    def __init__(self, n_ranks):
+        self.n_ranks = n_ranks
+        self.calls = []
+
+    def allreduce(self, values, op="sum"):
+        self.calls.append((list(values), op))
+        return list(values)
+
+
+def test_ranks_issue_collectives_only_across_processes_unless_forced():
+    # one process (plain run, or one rank): barrier / max / sum stay local
+    for mode, n in (("local", 1), ("local", 8), ("rank", 1)):
+        g = _FakeGroup(n)
+        r = bench.Ranks(g, mode)
+        r.barrier()
+        assert r.max(2.5) == 2.5 and r.sum(3.0) == 3.0 and g.calls == []
+    # ranks of a multi-process launch, and any group with --debug-force-collectives, go through RCCL
+    for mode, n, forced in (("rank", 2, False), ("local", 1, True), ("rank", 1, True)):
+        g = _FakeGroup(n)
+        r = bench.Ranks(g, mode, forced)
+        r.barrier()
+        r.max(1.0)
+        r.sum(1.0)
+        assert [op for _, op in g.calls] == ["sum", "max", "sum"]
