@@ -105,6 +105,7 @@ SIGNATURES = {
     "arx_set_seed": (C.c_int, [_P, C.c_uint64]),
     "arx_render": (C.c_int, [_P, _D]),
     "arx_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
+    "arx_set_timing": (C.c_int, [_P, C.c_int32]),
     "arx_clear_histogram": (C.c_int, [_P]),
     "arx_trace_rays": (C.c_int, [_P, C.c_uint64, C.c_uint64]),
     "arx_histogram_device": (C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_size_t)]),
@@ -172,6 +173,7 @@ SIGNATURES = {
     "arx_group_set_seed": (C.c_int, [_P, C.c_uint64]),
     "arx_group_render": (C.c_int, [_P, _D]),
     "arx_group_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
+    "arx_group_set_timing": (C.c_int, [_P, C.c_int32]),
     "arx_group_synchronize": (C.c_int, [_P]),
     "arx_group_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
     "arx_group_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),

@@ -1154,6 +1154,18 @@ arx_status arx_clear_histogram(arx_renderer* r) {
 }
 
 arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end) {
+    return r ? arx::trace_rays(r, ray_begin, ray_end, r->timing) : fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+}
+
+arx_status arx_set_timing(arx_renderer* r, int32_t on) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    r->timing = on != 0;
+    return ARX_OK;
+}
+
+}  // extern "C"
+
+arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (ray_end < ray_begin) return fail(ARX_ERR_INVALID_ARGUMENT, "ray_end < ray_begin");
     // global ray ids index the launch of N = x*y*z rays: energies are normalised by N and the
@@ -1249,12 +1261,16 @@ arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end)
     r->stats.trace_vgprs = r->occ[fmt][small][0];
     r->stats.trace_waves_per_simd = r->occ[fmt][small][1];
     r->stats.trace_waves_target = r->occ[fmt][small][2];
-    ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
+    if (timed) ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
     ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
-    ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
-    ++r->trace_launches;
+    if (timed) {
+        ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
+        ++r->trace_launches;
+    }
     return fif_done_one(r, r->ev_traced);
 }
+
+extern "C" {
 
 arx_status arx_finalize_ir(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
@@ -1272,7 +1288,7 @@ arx_status arx_finalize_ir(arx_renderer* r) {
 arx_status arx_render(arx_renderer* r, double* render_ms) {
     arx_status st = arx_clear_histogram(r);
     if (st != ARX_OK) return st;
-    st = arx_trace_rays(r, 0, n_rays(r->cfg));
+    st = arx::trace_rays(r, 0, n_rays(r->cfg), r->timing || render_ms != nullptr);
     if (st != ARX_OK) return st;
     st = arx_finalize_ir(r);
     if (st != ARX_OK) return st;
@@ -1479,12 +1495,14 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     if (st != ARX_OK) return st;
     const bool ir_new = r->conv_ir_dirty;
     const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
-    ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
+    if (r->timing) ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
     ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
                      ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
     r->conv_ir_dirty = false;
-    ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
-    ++r->conv_launches;
+    if (r->timing) {
+        ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
+        ++r->conv_launches;
+    }
     return fif_done_conv(r);
 }
 
@@ -1511,12 +1529,14 @@ arx_status arx_convolute_prepared(arx_renderer* r, float* d_out_left, float* d_o
     if (st != ARX_OK) return st;
     const bool ir_new = r->conv_ir_dirty;
     const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
-    ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
+    if (r->timing) ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
     ARX_HIP(conv_run_prepared(r->conv, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
                               ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
     r->conv_ir_dirty = false;
-    ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
-    ++r->conv_launches;
+    if (r->timing) {
+        ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
+        ++r->conv_launches;
+    }
     if (n_frames) *n_frames = (size_t)n;
     return fif_done_conv(r);
 }
@@ -1549,7 +1569,10 @@ arx_status arx_convolute_audio_file(arx_renderer* r, const float* h_in, size_t i
         r->conv_cap = n;
     }
     if (n > 0) ARX_HIP(hipMemcpyAsync(r->d_conv_in, h_in, n * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    const bool timing = r->timing;
+    r->timing = timing || conv_ms != nullptr;  // the convolution's own window when asked for
     arx_status st = arx_convolute_device(r, r->d_conv_in, n, r->d_conv_out, r->d_conv_out + n);
+    r->timing = timing;
     if (st != ARX_OK) return st;
     if (n > 0) {
         ARX_HIP(hipMemcpyAsync(h_out_left, r->d_conv_out, n * sizeof(float), hipMemcpyDeviceToHost, r->stream));

@@ -404,7 +404,7 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         uint64_t b = 0, e = 0;
         shard_of(n, g->rank0 + (int32_t)i, g->n_ranks, &b, &e);
         arx_status st = arx_clear_histogram(r);
-        if (st == ARX_OK) st = arx_trace_rays(r, b, e);
+        if (st == ARX_OK) st = trace_rays(r, b, e, r->timing || render_ms != nullptr);
         if (st != ARX_OK) return st;
     }
     // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:
@@ -494,6 +494,10 @@ arx_status arx_group_synchronize(arx_group* g) {
 
 arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n) {
     return for_all(g, [&](arx_renderer* r) { return arx_set_frames_in_flight(r, n); });
+}
+
+arx_status arx_group_set_timing(arx_group* g, int32_t on) {
+    return for_all(g, [&](arx_renderer* r) { return arx_set_timing(r, on); });
 }
 
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len) {

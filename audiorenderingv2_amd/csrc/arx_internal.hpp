@@ -86,6 +86,8 @@ struct arx_stream;
 namespace arx {
 // Device time (ms) of the renderer's last trace launch; wait = synchronise on it first.
 arx_status last_trace_ms(arx_renderer* r, bool wait, double* ms);
+// arx_trace_rays with the per-launch events recorded or not (arx_set_timing, or a caller asking for the time)
+arx_status trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed);
 // Install a built scene (arx_set_scene's second half): uploaded at the next trace.
 arx_status set_scene_image(arx_renderer* r, SceneRef img);
 // Frames in flight (arx_set_frames_in_flight): the current set's stream waits for the other set's
@@ -111,7 +113,8 @@ struct arx_renderer {
     // (arx_live_times)
     static constexpr int kTraceRing = 256;
     hipEvent_t tev0[kTraceRing] = {}, tev1[kTraceRing] = {};
-    uint64_t trace_launches = 0;
+    uint64_t trace_launches = 0;  // timed trace launches (the ring's index)
+    bool timing = true;           // arx_set_timing: record the per-launch events
     hipEvent_t cev0[kTraceRing] = {}, cev1[kTraceRing] = {};
     uint64_t conv_launches = 0;
     hipEvent_t lev0[kTraceRing] = {}, lev1[kTraceRing] = {};

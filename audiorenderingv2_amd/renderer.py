@@ -150,6 +150,11 @@ class AudioRenderer:
         convolution refers to the last frame started."""
         check(lib().arx_set_frames_in_flight(self._h, int(n)))
 
+    def set_timing(self, on: bool) -> None:
+        """arx_set_timing: per-launch timing events (trace_times / conv_times) on or off; a render()
+        still times its trace."""
+        check(lib().arx_set_timing(self._h, 1 if on else 0))
+
     def set_seed(self, seed: int) -> None:
         check(lib().arx_set_seed(self._h, int(seed)))
 
@@ -479,6 +484,10 @@ class RenderGroup:
     def set_frames_in_flight(self, n: int) -> None:
         """arx_group_set_frames_in_flight: AudioRenderer.set_frames_in_flight on every member."""
         check(lib().arx_group_set_frames_in_flight(self._g, int(n)))
+
+    def set_timing(self, on: bool) -> None:
+        """arx_group_set_timing: AudioRenderer.set_timing on every member."""
+        check(lib().arx_group_set_timing(self._g, 1 if on else 0))
 
     def set_seed(self, seed: int) -> None:
         check(lib().arx_group_set_seed(self._g, int(seed)))

@@ -289,6 +289,7 @@ def moving_listener_rank_shape(settings, scene, receiver, frames: int, shard: in
 
     r = AudioRenderer(settings, scene=scene, receiver=receiver)
     r.setEmitterPosInOptix(CONFERENCE_EMITTER)
+    r.set_timing(False)  # host wall clock per frame; no event markers in it
     x0, y0, z0 = CONFERENCE_LISTENER
     lat = []
     for k in range(frames + 3):
@@ -414,6 +415,9 @@ def main(argv=None) -> int:
                          "that chain with every collective forced on one GPU)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
+    ap.add_argument("--timing-events", action="store_true",
+                    help="keep the renderers' per-launch timing events on in the timed steps too (A/B of their cost; "
+                         "the kernel-times leg records them either way)")
     ap.add_argument("--no-host-leg", action="store_true",
                     help="skip the host-buffer (PCIe-inclusive) leg: render + arx_convolute_audio_file from and to "
                          "host memory")
@@ -469,6 +473,9 @@ def main(argv=None) -> int:
             g.debug_force_collectives(True, True)
         g.set_receiver_model(*receiver)
         g.set_scene(scene)  # the rank path: rank 0 builds, the tree reaches the other ranks over RCCL
+    # the timed steps carry no per-launch event markers (each cost its stream ~4.5 us,
+    # tools/step_gaps.py); the kernel times come from a leg of their own below
+    g.set_timing(args.timing_events)
     ranks = Ranks(g, plan["mode"], args.debug_force_collectives)
     ranks.barrier()
     if plan["mode"] == "rank" and rank == 0 and world > 1:
@@ -549,10 +556,23 @@ def main(argv=None) -> int:
         el1 = ranks.max(time.perf_counter() - t0s)
         q1 = int(round(ranks.sum(int(g.stats()["queries"]))))
         single_frame = {"value": q1 * args.steps / el1, "ms_per_step": el1 / args.steps * 1e3,
-                        "why": "the same steps with one frame in flight; the per-launch kernel times below "
-                               "(phases_ms_rank0, roofline) are this leg's"}
-    # the trace kernel's own window (direction pre-pass + trace kernel, HIP events on the
-    # renderer's stream) for each of the K timed launches of GPU 0 of this process
+                        "why": "the same steps with one frame in flight (no per-launch timing events, as in the "
+                               "timed steps)"}
+    # The per-launch kernel times: W + K more single-frame steps with the timing events on (HIP
+    # events on the renderer's stream around the direction pre-pass + trace kernel, and around the IR
+    # spectra + convolution), the K timed launches of GPU 0 of this process.
+    g.set_frames_in_flight(1)
+    g.set_timing(True)
+    for _ in range(args.warmup):
+        step()
+    g.synchronize()
+    ranks.barrier()
+    t0k = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    g.synchronize()
+    ranks.barrier()
+    timed_leg_ms = ranks.max(time.perf_counter() - t0k) / args.steps * 1e3
     trace_list = m0.trace_times(args.steps)
     assert len(trace_list) == args.steps, (len(trace_list), args.steps)
     trace_ms = float(np.mean(trace_list))
@@ -644,6 +664,7 @@ def main(argv=None) -> int:
             g5.set_receiver_model(*receiver)
             g5.set_scene(scene)
         g5.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        g5.set_timing(False)  # host wall clock per frame; no event markers in it
         moving = moving_listener(g5, ranks, args.c5_frames, int(np.prod(C5["rays"])) // world)
         g5.close()
     bpb = bytes_per_bounce(n_tris)
@@ -694,6 +715,12 @@ def main(argv=None) -> int:
                                         "(a one-rank group skips them unless forced)"),
         "setup_s_rank0": setup_s,
         "single_frame": single_frame,
+        "kernel_times_leg": {"steps": args.steps, "warmup": args.warmup, "frames_in_flight": 1,
+                             "ms_per_step": timed_leg_ms,
+                             "why": "W + K more single-frame steps with the renderer's per-launch HIP events on "
+                                    "(arx_set_timing): phases_ms_rank0 and the rooflines are this leg's launches; "
+                                    "its step time against single_frame's is what the four event markers cost a "
+                                    "step"},
         "preroll": {"steps": pre_steps, "seconds_rank0": preroll_s,
                     "why": "untimed steps before the W warmup steps, until the GPU runs at its sustained clock "
                            "(a fresh or idle MI355X ramps over its first ~10 C3 launches, 2.95 -> 2.67 ms; "

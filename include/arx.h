@@ -183,6 +183,13 @@ arx_status arx_conv_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out);
 /* Capacity of the per-launch timing rings above (launches kept). */
 int32_t arx_timing_ring(void);
+/* Per-launch timing on (1, the default) or off (0).  Each timed launch puts two event markers on the
+ * stream, ~4.5 us of stream time apiece on MI355X (tools/step_gaps.py): off, trace and file
+ * convolution launches go to the stream alone and the rings above stop growing.  A call that asks
+ * for its time -- arx_render / arx_group_render with render_ms, arx_convolute_audio_file with
+ * convolute_ms -- is timed either way, as the reference times render() only when render_ms is given
+ * (AudioRenderer.h:27). */
+arx_status arx_set_timing(arx_renderer* r, int32_t on);
 
 /* Identity of the trace kernel compiled into this library: a hash of its sources and experiment
  * macros (build.py trace_source_id).  Stored PMC profiles carry it with the tree hash and VGPR
@@ -261,6 +268,8 @@ arx_status arx_group_render(arx_group* g, double* render_ms);
  * frames, in and out of place, bit-identical to a plain renderer); its first multi-GPU run is the
  * 8-GPU bench, which keeps the one-GPU frames-in-flight policy at every N. */
 arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n);
+/* arx_set_timing on every member. */
+arx_status arx_group_set_timing(arx_group* g, int32_t on);
 arx_status arx_group_synchronize(arx_group* g);
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
 /* Queries / receiver hits / misses summed over this process's members; times = the longest. */
