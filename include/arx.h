@@ -188,7 +188,7 @@ int32_t arx_timing_ring(void);
  * convolution launches go to the stream alone and the rings above stop growing.  A call that asks
  * for its time -- arx_render / arx_group_render with render_ms, arx_convolute_audio_file with
  * convolute_ms -- is timed either way, as the reference times render() only when render_ms is given
- * (AudioRenderer.h:27). */
+ * (AudioRenderer.h:27).  arx_get_stats' trace_ms / conv_ms then report the last timed launch. */
 arx_status arx_set_timing(arx_renderer* r, int32_t on);
 
 /* Identity of the trace kernel compiled into this library: a hash of its sources and experiment
