@@ -1133,6 +1133,15 @@ arx_status arx_set_seed(arx_renderer* r, uint64_t seed) {
 
 arx_status arx_clear_histogram(arx_renderer* r) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+    const arx_status st = arx::begin_frame(r);
+    if (st != ARX_OK) return st;
+    ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
+    return ARX_OK;
+}
+
+}  // extern "C"
+
+arx_status arx::begin_frame(arx_renderer* r) {
     ARX_HIP(hipSetDevice(r->cfg.device));
     if (r->fif > 1) {  // a frame starts: it takes the next set's stream, histogram, IR, counters and directions
         arx_renderer::FrameSet cur{r->own_stream, r->d_hist, r->d_ir, r->d_counters, r->h_counters, r->d_dirs, r->dirs_cap};
@@ -1149,9 +1158,10 @@ arx_status arx_clear_histogram(arx_renderer* r) {
         r->alt[r->fif - 2] = cur;
         r->slot = (r->slot + 1) % r->fif;
     }
-    ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
     return ARX_OK;
 }
+
+extern "C" {
 
 arx_status arx_trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end) {
     return r ? arx::trace_rays(r, ray_begin, ray_end, r->timing) : fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
@@ -1165,7 +1175,7 @@ arx_status arx_set_timing(arx_renderer* r, int32_t on) {
 
 }  // extern "C"
 
-arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed) {
+arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed, bool clear) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (ray_end < ray_begin) return fail(ARX_ERR_INVALID_ARGUMENT, "ray_end < ray_begin");
     // global ray ids index the launch of N = x*y*z rays: energies are normalised by N and the
@@ -1212,7 +1222,14 @@ arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end
     a.delay = (int32_t)((double)c.sample_rate * 0.00044);  // devicePrograms.cu:125
     a.is_mono = c.is_mono;
     a.bvh_depth = r->stats.bvh_depth;
-    if (ray_end == ray_begin) return ARX_OK;
+    if (clear) {
+        a.clear_bins = 2 * (uint64_t)r->ir_len;
+        a.clear_counters = kCounters;
+    }
+    if (ray_end == ray_begin) {  // nothing to trace: the clear alone
+        if (clear) ARX_HIP(launch_clear(r->hist(), 2 * (uint64_t)r->ir_len, r->d_counters, (int)kCounters, r->stream));
+        return ARX_OK;
+    }
     if (ray_end - ray_begin > r->dirs_cap) {  // direction pre-pass buffer
         if (r->d_dirs) ARX_HIP(hipFree(r->d_dirs));
         r->d_dirs = nullptr;
@@ -1286,9 +1303,16 @@ arx_status arx_finalize_ir(arx_renderer* r) {
 }
 
 arx_status arx_render(arx_renderer* r, double* render_ms) {
+    if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
+#ifdef ARX_EXP_SEPARATE_CLEAR  // design experiments only: the clear as a launch of its own (round-5 A/B)
     arx_status st = arx_clear_histogram(r);
     if (st != ARX_OK) return st;
-    st = arx::trace_rays(r, 0, n_rays(r->cfg), r->timing || render_ms != nullptr);
+    st = arx::trace_rays(r, 0, n_rays(r->cfg), r->timing || render_ms != nullptr, false);
+#else
+    arx_status st = arx::begin_frame(r);  // the clear rides on the direction pre-pass
+    if (st != ARX_OK) return st;
+    st = arx::trace_rays(r, 0, n_rays(r->cfg), r->timing || render_ms != nullptr, true);
+#endif
     if (st != ARX_OK) return st;
     st = arx_finalize_ir(r);
     if (st != ARX_OK) return st;

@@ -403,8 +403,8 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         arx_renderer* r = g->members[i];
         uint64_t b = 0, e = 0;
         shard_of(n, g->rank0 + (int32_t)i, g->n_ranks, &b, &e);
-        arx_status st = arx_clear_histogram(r);
-        if (st == ARX_OK) st = trace_rays(r, b, e, r->timing || render_ms != nullptr);
+        arx_status st = begin_frame(r);  // the clear rides on the direction pre-pass
+        if (st == ARX_OK) st = trace_rays(r, b, e, r->timing || render_ms != nullptr, true);
         if (st != ARX_OK) return st;
     }
     // 2. the exchange step: int64 SUM of the histograms (a group of one rank has nothing to sum:

@@ -86,8 +86,12 @@ struct arx_stream;
 namespace arx {
 // Device time (ms) of the renderer's last trace launch; wait = synchronise on it first.
 arx_status last_trace_ms(arx_renderer* r, bool wait, double* ms);
-// arx_trace_rays with the per-launch events recorded or not (arx_set_timing, or a caller asking for the time)
-arx_status trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed);
+// arx_trace_rays with the per-launch events recorded or not (arx_set_timing, or a caller asking for the
+// time); clear: the direction pre-pass zeroes the histogram and counters first (render() after
+// begin_frame, instead of arx_clear_histogram's launch)
+arx_status trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end, bool timed, bool clear = false);
+// arx_clear_histogram without its launch: with frames in flight, the next frame takes the next set
+arx_status begin_frame(arx_renderer* r);
 // Install a built scene (arx_set_scene's second half): uploaded at the next trace.
 arx_status set_scene_image(arx_renderer* r, SceneRef img);
 // Frames in flight (arx_set_frames_in_flight): the current set's stream waits for the other set's

@@ -146,6 +146,8 @@ struct TraceArgs {
     unsigned long long* cursor;  // the launch's ray-pool cursor (reset by the direction pre-pass)
     uint32_t dyn_share;          // rays in the pool: n * dyn_share / 256 (set by launch_trace)
     uint32_t dyn_chunk;          // rays per pool atomic
+    uint64_t clear_bins;         // > 0: the direction pre-pass also zeroes hist[0, clear_bins) ...
+    int32_t clear_counters;      // ... and counters[0, clear_counters) (render(): no separate clear launch)
 };
 // Node formats of the trace kernel (arx_stats::trace_format)
 constexpr int kFmtF32 = 0, kFmtQ16 = 1, kFmtW4 = 2;

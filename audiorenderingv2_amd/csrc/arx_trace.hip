@@ -1001,10 +1001,16 @@ __global__ void clear_kernel(unsigned long long* __restrict__ hist, uint64_t n, 
     if (i < (uint64_t)n_counters) counters[i] = 0ull;
 }
 
-// Direction pre-pass: float4(dir, 0) for rays [first, first + count).
-__global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out, unsigned long long* cursor) {
+// Direction pre-pass: float4(dir, 0) for rays [first, first + count); with clear_bins > 0 it also
+// zeroes the histogram and the counters the trace accumulates into (render(): one launch fewer per
+// frame, and the kernel boundary it cost).
+__global__ void dirs_kernel(uint64_t seed, uint64_t first, uint64_t count, float4* out, unsigned long long* cursor,
+                            unsigned long long* __restrict__ hist, uint64_t clear_bins,
+                            unsigned long long* __restrict__ counters, int clear_counters) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *cursor = 0ull;  // the trace launch's chunk pool (trace_kernel) starts empty-handed
+    if (i < clear_bins) hist[i] = 0ull;
+    if (i < (uint64_t)clear_counters) counters[i] = 0ull;
     if (i >= count) return;
     const float3 d = ray_direction(seed, first + i);
     out[i] = make_float4(d.x, d.y, d.z, 0.0f);
@@ -1086,8 +1092,10 @@ hipError_t launch(const TraceArgs& args, int cus, hipStream_t s) {
     const bool dyn = uses_pool<FMT, GSTACK>(args, cus);
     a2.dyn_share = dyn ? (uint32_t)kDynShare : 0u;
     a2.dyn_chunk = (uint32_t)kDynChunk;
-    hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((n_rays + 255) / 256)), dim3(256), 0, s, args.seed,
-                       args.ray_begin, n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor);
+    const uint64_t pre = std::max<uint64_t>(n_rays, args.clear_bins);
+    hipLaunchKernelGGL(dirs_kernel, dim3((unsigned)((pre + 255) / 256)), dim3(256), 0, s, args.seed, args.ray_begin,
+                       n_rays, reinterpret_cast<float4*>(const_cast<void*>(args.dirs)), args.cursor, args.hist,
+                       args.clear_bins, args.counters, args.clear_counters);
     if (kSmallBlock > 0 && !dyn) {
         // Small launches (about a ray per lane: C2, one 8-GPU rank's C5 shard) in 4-wave blocks,
         // one wave per SIMD each: 0.465 -> 0.44 ms at C2

@@ -9,7 +9,7 @@ recover), from a rocprofv3 kernel trace.
 
 A step = render (clear, direction pre-pass, trace, finalize) + the file convolution (IR spectra and
 the three passes), all on the renderer's stream.  The analysis takes the last `steps` steps (each
-begins with the clear launch), and per step reports the wall span from the first kernel's start to
+begins with the direction pre-pass, or the histogram clear before it), and per step reports the wall span from the first kernel's start to
 the last one's end, the kernels' summed durations and the difference: the time the stream spent
 between kernels.
 """
@@ -58,7 +58,12 @@ def run(workload: str, steps: int) -> None:
 def analyze(trace_csv: str, steps: int) -> None:
     rows = [r for r in csv.DictReader(open(trace_csv)) if "arx::" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "clear_kernel" in r["Kernel_Name"]]
+    # a step begins with its direction pre-pass, or with the histogram clear right before it (builds
+    # whose render() still launches the clear separately)
+    starts = []
+    for i, r in enumerate(rows):
+        if "dirs_kernel" in r["Kernel_Name"]:
+            starts.append(i - 1 if i > 0 and "clear_kernel" in rows[i - 1]["Kernel_Name"] else i)
     starts = starts[-(steps + 1):]  # step k = [starts[k], starts[k + 1])
     spans, busy, per_kernel, gaps = [], [], {}, {}
     for a, b in zip(starts, starts[1:]):
