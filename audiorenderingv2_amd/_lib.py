@@ -128,6 +128,8 @@ SIGNATURES = {
     "arx_debug_ray_directions": (C.c_int, [C.c_uint64, C.c_uint64, C.c_uint64, _F, C.c_int]),
     "arx_debug_trace_counters": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t]),
     "arx_debug_set_trace_path": (C.c_int, [_P, C.c_int]),
+    "arx_debug_set_refit_pad": (C.c_int, [_P, C.c_float]),
+    "arx_debug_check_tree_limits": (C.c_int, [C.c_uint64, C.c_uint64]),
     "arx_debug_wide_stats": (C.c_int, [_F, _F, C.c_int64, _F, C.c_int64, C.c_int32, C.c_uint64, _D, C.c_size_t]),
     "arx_debug_trace_profile": (C.c_int, [_P, C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_debug_node_images": (C.c_int, [_P, _P, _P, C.c_size_t, _F, C.POINTER(C.c_uint64)]),
@@ -136,6 +138,7 @@ SIGNATURES = {
     "arx_live_times": (C.c_int, [_P, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
     "arx_timing_ring": (C.c_int32, []),
     "arx_trace_kernel_id": (C.c_uint64, []),
+    "arx_conv_kernel_id": (C.c_uint64, []),
     "arx_debug_set_leaf_max": (C.c_int, [C.c_int32]),
     "arx_device_count": (C.c_int32, []),
     "arx_device_alloc": (C.c_int, [C.c_int32, C.c_size_t, C.POINTER(_P)]),
@@ -174,6 +177,11 @@ SIGNATURES = {
     "arx_group_render": (C.c_int, [_P, _D]),
     "arx_group_set_frames_in_flight": (C.c_int, [_P, C.c_int32]),
     "arx_group_set_timing": (C.c_int, [_P, C.c_int32]),
+    "arx_group_allreduce_times": (C.c_int, [_P, C.c_int32, _D, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "arx_group_convolute_device": (C.c_int, [_P, C.POINTER(_P), C.c_size_t, C.POINTER(_P), C.POINTER(_P)]),
+    "arx_group_conv_shard": (None, [C.c_int32, C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint64)]),
+    "arx_group_conv_sharded": (C.c_int32, [_P]),
     "arx_group_synchronize": (C.c_int, [_P]),
     "arx_group_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
     "arx_group_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),

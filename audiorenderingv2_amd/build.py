@@ -59,18 +59,32 @@ def _newest(paths: list[str]) -> float:
 MEASUREMENT_MACROS = ("ARX_TRACE_COUNT", "ARX_TRACE_PROF")
 
 
-def trace_source_id(defines: tuple[str, ...] = ()) -> str:
-    """64-bit identity of the trace kernel a build compiles: a hash of its source files and of the
-    experiment macros (not the measurement-only ones).  Compiled into the library
-    (arx_trace_kernel_id) and stored in every PMC profile's guard, so bench.py uses a stored
-    profile only for the kernel it was taken of."""
+def _source_id(files: tuple[str, ...], defines: tuple[str, ...]) -> str:
     h = hashlib.sha1()
-    for f in ("arx_trace.hip", "arx_layout.hpp", "arx_kernels.hpp"):
+    for f in files:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
     for d in sorted(d for d in defines if d.split("=")[0] not in MEASUREMENT_MACROS):
         h.update(b"\0" + d.encode())
     return "0x" + h.hexdigest()[:16] + "ull"
+
+
+def trace_source_id(defines: tuple[str, ...] = ()) -> str:
+    """64-bit identity of the trace kernel a build compiles: a hash of its source files and of the
+    experiment macros (not the measurement-only ones).  Compiled into the library
+    (arx_trace_kernel_id) and stored in every PMC profile's guard, so bench.py uses a stored
+    profile only for the kernel it was taken of."""
+    # arx_kernels.hpp (host launcher declarations) is not part of it: its edits do not change the kernel
+    return _source_id(("arx_trace.hip", "arx_layout.hpp"), defines)
+
+
+def conv_source_id(defines: tuple[str, ...] = ()) -> str:
+    """The same identity for the file convolution's kernels (arx_conv.hip; arx_conv_kernel_id): the
+    guard of the stored convolution traffic profile."""
+    return _source_id(("arx_conv.hip",), defines)
+
+
+SOURCE_IDS = {"arx_trace.hip": ("ARX_TRACE_SRC_ID", trace_source_id), "arx_conv.hip": ("ARX_CONV_SRC_ID", conv_source_id)}
 
 
 def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = (), flags: tuple[str, ...] = ()) -> str:
@@ -79,7 +93,8 @@ def _compile(src: str, objdir: str = OBJDIR, defines: tuple[str, ...] = (), flag
     if os.path.exists(obj) and os.path.getmtime(obj) >= _newest(deps):
         return obj
     lang = ["-x", "hip"]  # host-only TUs too: they use the HIP runtime headers
-    extra = [f"-DARX_TRACE_SRC_ID={trace_source_id(defines)}"] if os.path.basename(src) == "arx_trace.hip" else []
+    sid = SOURCE_IDS.get(os.path.basename(src))
+    extra = [f"-D{sid[0]}={sid[1](defines)}"] if sid else []
     cmd = [hipcc(), *lang, *COMMON, *FILE_FLAGS.get(os.path.basename(src), []), *[f"-D{d}" for d in defines], *extra,
            *flags, "-c", src, "-o", obj]
     res = subprocess.run(cmd, capture_output=True, text=True)

@@ -274,6 +274,7 @@ arx_status ensure_device_scene(arx_renderer* r) {
         // flight may still be tracing
         const arx_status st = fif_wait_traced(r);
         if (st != ARX_OK) return st;
+        ++r->tree_gen;  // this write's off-grid flag value (arx_renderer::d_tree_flag)
     }
     const SceneImage& img = *r->scene_img;
     const BvhBuild& sc = img.bvh;
@@ -460,11 +461,9 @@ arx_status ensure_device_scene(arx_renderer* r) {
         // coded nodes on the device; on the refit path the refit below writes the receiver's
         // quantized nodes itself (its coded ones may not exist yet)
         const size_t nq = host_recv ? n_nodes : 1 + sc.nodes.size();
-        ARX_HIP(launch_requant16(r->d_cnodes, nq, r->qgrid, r->d_qnodes,
-                                 reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
+        ARX_HIP(launch_requant16(r->d_cnodes, nq, r->qgrid, r->d_qnodes, r->d_tree_flag, r->tree_gen, r->stream));
         if (r->use_w4)
-            ARX_HIP(launch_requant_w4(r->d_w4f, r->n_w4f, r->qgrid, r->d_wbuf,
-                                      reinterpret_cast<unsigned int*>(r->d_counters + 6), r->stream));
+            ARX_HIP(launch_requant_w4(r->d_w4f, r->n_w4f, r->qgrid, r->d_wbuf, r->d_tree_flag, r->tree_gen, r->stream));
         ++r->requants;
     }
     r->q_valid = recv_empty || qgrid_contains(r->qgrid, rlo, rhi);
@@ -485,12 +484,14 @@ arx_status ensure_device_scene(arx_renderer* r) {
         a.root_count = r->recv.root.count;
         receiver_rotation(r->yaw, a.m);
         for (int k = 0; k < 3; ++k) a.t[k] = r->center[k];
-        a.pad = refit_pad(r);  // >= the builder's pad; receiver_bound covers it
+        // >= the builder's pad; receiver_bound covers it (a debug pad does not: the off-grid test)
+        a.pad = r->debug_refit_pad > 0.0f ? r->debug_refit_pad : refit_pad(r);
         a.grid = r->qgrid;
         a.tris = r->d_tris;
         a.cnodes = r->d_cnodes;
         a.qnodes = r->q_valid ? r->d_qnodes : nullptr;
-        a.flag = reinterpret_cast<unsigned int*>(r->d_counters + 6);
+        a.flag = r->d_tree_flag;
+        a.flag_value = r->tree_gen;
         if (r->q_valid && r->use_w4) {  // the opt-in CW4 copy follows the quantized one (same grid)
             a.wbuf = r->d_wbuf;
             a.w4_nodes = r->d_recv_w4;
@@ -794,6 +795,7 @@ arx_status arx_live_times(arx_renderer* r, double* ms, size_t n, size_t* n_out) 
 
 int32_t arx_timing_ring(void) { return arx_renderer::kTraceRing; }
 uint64_t arx_trace_kernel_id(void) { return trace_kernel_source_id(); }
+uint64_t arx_conv_kernel_id(void) { return conv_kernel_source_id(); }
 
 arx_status arx_debug_set_leaf_max(int32_t leaf_max) {
     if (leaf_max < 1 || leaf_max > 15) return fail(ARX_ERR_INVALID_ARGUMENT, "leaf_max %d outside [1, 15]", leaf_max);
@@ -962,7 +964,9 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
         (e = hipMalloc(&r->d_hist, 2 * (size_t)r->ir_len * sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc(&r->d_ir, 2 * (size_t)r->ir_len * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&r->d_counters, (kCursor + 1) * sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipHostMalloc(&r->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess)
+        (e = hipHostMalloc(&r->h_counters, kCounters * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMalloc(&r->d_tree_flag, sizeof(unsigned int))) != hipSuccess ||
+        (e = hipHostMalloc(&r->h_tree_flag, sizeof(unsigned int), hipHostMallocDefault)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     r->stream = r->own_stream;
     for (int i = 0; i < arx_renderer::kTraceRing; ++i)
@@ -986,6 +990,7 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(r->d_tree_flag, 0, sizeof(unsigned int), r->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(r->stream)) != hipSuccess)
         return cleanup(fail(ARX_ERR_HIP, "arx_create: %s", hipGetErrorString(e)));
     *out = r;
@@ -1025,6 +1030,8 @@ void arx_destroy(arx_renderer* r) {
     hipFree(r->d_hist);
     hipFree(r->d_ir);
     hipFree(r->d_counters);
+    hipFree(r->d_tree_flag);
+    if (r->h_tree_flag) hipHostFree(r->h_tree_flag);
     hipFree(r->d_conv_in);
     hipFree(r->d_conv_out);
     if (r->h_counters) hipHostFree(r->h_counters);
@@ -1405,6 +1412,7 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     ARX_HIP(hipSetDevice(r->cfg.device));
     ARX_HIP(hipMemcpyAsync(r->h_counters, r->d_counters, kCounters * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                            r->stream));
+    ARX_HIP(hipMemcpyAsync(r->h_tree_flag, r->d_tree_flag, sizeof(unsigned int), hipMemcpyDeviceToHost, r->stream));
     ARX_HIP(hipStreamSynchronize(r->stream));
     r->stats.queries = r->h_counters[0];
     r->stats.receiver_hits = r->h_counters[1];
@@ -1416,7 +1424,9 @@ arx_status arx_get_stats(arx_renderer* r, arx_stats* out) {
     if (r->conv_launches > 0 && hipEventElapsedTime(&cms, r->cev0[cslot], r->cev1[cslot]) == hipSuccess)
         r->stats.conv_ms = cms;
     *out = r->stats;
-    if (r->h_counters[6]) return fail(ARX_ERR_INTERNAL, "receiver refit: a box left the quantization grid");
+    // the tree as last written (generation tree_gen) has a box off the quantization grid
+    if (r->tree_gen != 0 && *r->h_tree_flag == r->tree_gen)
+        return fail(ARX_ERR_INTERNAL, "receiver refit / re-quantization: a box left the quantization grid");
     return ARX_OK;
 }
 
@@ -1510,6 +1520,13 @@ arx_status arx_conv_describe(arx_renderer* r, int which, char* buf, size_t len) 
 
 arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
                                 float* d_out_right) {
+    return arx::convolute_pairs(r, d_in, n_frames, d_out_left, d_out_right, 0, INT64_MAX);
+}
+
+}  // extern "C"
+
+arx_status arx::convolute_pairs(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left,
+                                float* d_out_right, int64_t pair_begin, int64_t pair_end) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
     if (n_frames > 0 && (!d_in || !d_out_left || !d_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
     ARX_HIP(hipSetDevice(r->cfg.device));
@@ -1520,8 +1537,8 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     const bool ir_new = r->conv_ir_dirty;
     const int slot = (int)(r->conv_launches % arx_renderer::kTraceRing);
     if (r->timing) ARX_HIP(hipEventRecord(r->cev0[slot], r->stream));
-    ARX_HIP(conv_run(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
-                     ir_new ? r->d_ir + r->ir_len : nullptr, r->stream));
+    ARX_HIP(conv_run_pairs(r->conv, d_in, (int64_t)n_frames, d_out_left, d_out_right, ir_new ? r->d_ir : nullptr,
+                           ir_new ? r->d_ir + r->ir_len : nullptr, pair_begin, pair_end, r->stream));
     r->conv_ir_dirty = false;
     if (r->timing) {
         ARX_HIP(hipEventRecord(r->cev1[slot], r->stream));
@@ -1529,6 +1546,12 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
     }
     return fif_done_conv(r);
 }
+
+bool arx::conv_shards(arx_renderer* r) {
+    return ensure_conv(r, false) == ARX_OK && conv_plan_shards(r->conv);
+}
+
+extern "C" {
 
 arx_status arx_convolute_prepare_input(arx_renderer* r, const float* d_in, size_t n_frames) {
     if (!r) return fail(ARX_ERR_INVALID_ARGUMENT, "renderer is NULL");
@@ -1682,6 +1705,17 @@ arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_word
     const size_t k = std::min(n_words, r->prof_words);
     ARX_HIP(hipMemcpy(out, r->d_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
     if (n_out) *n_out = k;
+    return ARX_OK;
+}
+
+arx_status arx_debug_check_tree_limits(uint64_t n_nodes, uint64_t n_tris) {
+    return check_buffer_offsets((size_t)n_nodes, (size_t)n_tris);
+}
+
+arx_status arx_debug_set_refit_pad(arx_renderer* r, float pad) {
+    if (!r || !(pad >= 0.0f) || !std::isfinite(pad)) return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    r->debug_refit_pad = pad;
+    r->recv_pose_dirty = true;  // the next trace refits with it
     return ARX_OK;
 }
 

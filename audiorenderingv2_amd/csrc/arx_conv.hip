@@ -347,6 +347,12 @@ struct PassArgs {
     const double* in_d;  // live block input (f64)
     int64_t n_in;        // live block length (<= block length of the plan)
     double* out_d;       // live output, interleaved L/R, 2*n doubles
+    // chained pass C of a time-block shard (conv_run_pairs): the first local pair whose output
+    // segments are written (1 when local pair 0 is the seam pair, re-transformed only for its
+    // second block's tail), and whether the segment after the last pair is this shard's (the file's
+    // last shard)
+    int32_t emit_from;
+    int32_t tail;
 };
 
 // Pass A: forward column FFTs.  mode 0: batch = block pair p; mode 1: batch = IR channel c.
@@ -1304,7 +1310,7 @@ __device__ __forceinline__ void pass_c_chain_body(const MrArgs& m) {
     const PassArgs& a = m.p;
     const int nt = blockDim.x, tc = nt >> 6, lgc = __builtin_ctz(tc), N1 = a.N1, N2 = a.N2, half = N1 >> 1;
     const int ch = blockIdx.y & 1;
-    const int64_t p0 = (int64_t)(blockIdx.y >> 1) * m.chain;
+    const int64_t p0 = a.emit_from + (int64_t)(blockIdx.y >> 1) * m.chain;
     const int64_t p1 = p0 + m.chain < a.n_pairs ? p0 + m.chain : a.n_pairs;
     const int n2_0 = xcd_tile(blockIdx.x, gridDim.x) * tc, sc = mr_col_stride(N1, tc);
     double2* twl = lds + (size_t)tc * sc;
@@ -1375,7 +1381,7 @@ __device__ __forceinline__ void pass_c_chain_body(const MrArgs& m) {
         }
         __syncthreads();  // the tile is rewritten by the next pair
     }
-    if (p1 == a.n_pairs) {  // the segment after the last pair: F_last alone
+    if (p1 == a.n_pairs && a.tail) {  // the segment after the last pair: F_last alone
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int i = threadIdx.x + it * nt;
@@ -1552,6 +1558,8 @@ static PassArgs base_args(const ConvPlan* p) {
     a.H = p->d_H;
     a.G = p->d_G;
     a.ylen = plan_ylen(p);
+    a.emit_from = 0;
+    a.tail = 1;
     return a;
 }
 
@@ -1658,7 +1666,7 @@ static void mr_pass_c(const ConvPlan* p, const PassArgs& a, int64_t pairs, hipSt
     MrArgs m = mr_args(p, a);
     if (p->n == 2 * p->sr && p->N1 % 2 == 0) {  // inverse columns and seams in one pass
         m.chain = ARX_CONV_CHAIN;
-        const unsigned chains = (unsigned)((pairs + m.chain - 1) / m.chain);
+        const unsigned chains = (unsigned)((pairs - a.emit_from + m.chain - 1) / m.chain);
         if constexpr (L1 > 0)
             hipLaunchKernelGGL((pass_c_chain3<R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCC), 2 * chains),
                                dim3(64 * ARX_CONV_TCC), mr_lds_c(p, ARX_CONV_TCC), s, m);
@@ -1735,23 +1743,62 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
     return hipGetLastError();
 }
 
+// The chained pass C (inverse columns and seams in one pass, no block windows in HBM): n = 2 sr on the
+// direct path with N1 even.  Only these plans convolve a time-block shard on its own.
+static bool chain_plan(const ConvPlan* p) { return p->direct && p->n == 2 * p->sr && p->N1 % 2 == 0; }
+
+bool conv_plan_shards(const ConvPlan* p) { return p && chain_plan(p); }
+
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
                     const float* d_ir_left, const float* d_ir_right, hipStream_t s) {
+    return conv_run_pairs(p, d_in, n_frames, d_out_left, d_out_right, d_ir_left, d_ir_right, 0, INT64_MAX, s);
+}
+
+// conv_run restricted to the block pairs [pair_begin, pair_end) (time blocks sharded
+// across GPUs).  On a chained plan the shard runs passes A and B over its pairs plus the pair before
+// them (the seam: its second block's tail F, re-made here instead of received from the neighbour) and
+// pass C emits exactly the output segments of its own pairs -- the same per-pair arithmetic in the
+// same summation order as the whole file's chains (which re-make the previous pair at every chain
+// boundary already), so the union of the shards is the whole convolution bit for bit.  Other plans
+// convolve the whole file (every frame written).
+hipError_t conv_run_pairs(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
+                          const float* d_ir_left, const float* d_ir_right, int64_t pair_begin, int64_t pair_end,
+                          hipStream_t s) {
     const bool with_ir = d_ir_left && d_ir_right;
     if (with_ir && (!p->direct || n_frames < p->sr)) {  // spectra first, then the audio
         const hipError_t e = conv_set_ir(p, d_ir_left, d_ir_right, s);
         if (e != hipSuccess) return e;
-        return conv_run(p, d_in, n_frames, d_out_left, d_out_right, nullptr, nullptr, s);
+        return conv_run_pairs(p, d_in, n_frames, d_out_left, d_out_right, nullptr, nullptr, pair_begin, pair_end, s);
     }
     if (n_frames <= 0) return hipSuccess;
     p->prepared = false;  // any other file convolution discards a prepared input (pass A overwrites its spectra)
-    const int64_t S = n_frames / p->sr;  // kernels.cu:413
+    int64_t S = n_frames / p->sr;  // kernels.cu:413
     if (S == 0) {  // nothing convolved: the reference output stays zero
         hipError_t e = hipMemsetAsync(d_out_left, 0, (size_t)n_frames * sizeof(float), s);
         if (e == hipSuccess) e = hipMemsetAsync(d_out_right, 0, (size_t)n_frames * sizeof(float), s);
         return e;
     }
-    const int64_t pairs = (S + 1) / 2;
+    const int64_t all_pairs = (S + 1) / 2;
+    int64_t base = 0, pairs = all_pairs;  // local pair 0 = global pair `base`
+    int32_t emit_from = 0, tail = 1;
+    if (chain_plan(p) && (pair_begin > 0 || pair_end < all_pairs)) {
+        const int64_t pb = std::max<int64_t>(0, std::min(pair_begin, all_pairs));
+        const int64_t pe = std::max<int64_t>(pb, std::min(pair_end, all_pairs));
+        if (pe == pb) {  // an empty shard: its IR spectra still follow the IR
+            if (!with_ir) return hipSuccess;
+            return conv_set_ir(p, d_ir_left, d_ir_right, s);
+        }
+        base = pb > 0 ? pb - 1 : 0;
+        emit_from = pb > 0 ? 1 : 0;
+        tail = pe == all_pairs ? 1 : 0;
+        pairs = pe - base;
+        const int64_t off = 2 * base * (int64_t)p->sr;
+        d_in += off;
+        d_out_left += off;
+        d_out_right += off;
+        n_frames -= off;
+        S = std::min<int64_t>(S - 2 * base, 2 * pairs);
+    }
     const int64_t ylen = plan_ylen(p);
     // the chained pass C (mr_file) keeps the block windows on chip: no Y
     const bool windows = !(p->direct && p->n == 2 * p->sr && p->N1 % 2 == 0);
@@ -1782,6 +1829,8 @@ hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_o
     a.scale = (double)p->n / ((double)p->M * (double)(p->n / 2));  // AudioRenderer.cpp:709
     a.ir_l = d_ir_left;
     a.ir_r = d_ir_right;
+    a.emit_from = emit_from;
+    a.tail = tail;
     const size_t lds_a = ((size_t)p->tc + 1) * p->N1 * sizeof(double2);  // + the twiddle table
     if (p->direct) {
         mr_dispatch(p, [&](auto r7, auto lm, auto l1, auto l2) {
@@ -2137,6 +2186,11 @@ hipError_t stream_run(StreamPlan* p, const double* d_in, int64_t n_in, double* d
     ++p->blocks;
     return hipGetLastError();
 }
+
+#ifndef ARX_CONV_SRC_ID
+#define ARX_CONV_SRC_ID 0ull  // set by build.py: hash of this file's sources and experiment macros
+#endif
+uint64_t conv_kernel_source_id() { return ARX_CONV_SRC_ID; }
 
 int32_t stream_plan_block(const StreamPlan* p) { return p ? p->B : 0; }
 int32_t stream_plan_partitions(const StreamPlan* p) { return p ? p->P : 0; }

@@ -49,6 +49,14 @@ struct arx_group {
     // collectives the group issued (arx_debug_group_collectives): [0] histogram all-reduces, [1] f64
     // all-reduces, [2] scene broadcasts (rank path)
     uint64_t n_coll[3] = {0, 0, 0};
+    // per member: HIP events around its histogram all-reduce (recorded when the member's timing is on
+    // or render_ms is asked for), a ring like the renderer's trace ring (arx_group_allreduce_times)
+    static constexpr int kRing = 256;
+    struct ArEvents {
+        hipEvent_t e0[kRing] = {}, e1[kRing] = {};
+        uint64_t n = 0;
+    };
+    std::vector<ArEvents> ar;
 };
 
 namespace {
@@ -73,6 +81,14 @@ void destroy_members(arx_group* g) {
         hipSetDevice(g->members[i]->cfg.device);
         if (g->traced[i]) hipEventDestroy(g->traced[i]);
     }
+    for (size_t i = 0; i < g->ar.size(); ++i) {
+        hipSetDevice(g->members[i]->cfg.device);
+        for (int k = 0; k < arx_group::kRing; ++k) {
+            if (g->ar[i].e0[k]) hipEventDestroy(g->ar[i].e0[k]);
+            if (g->ar[i].e1[k]) hipEventDestroy(g->ar[i].e1[k]);
+        }
+    }
+    g->ar.clear();
     if (g->summed) {
         hipSetDevice(g->members[0]->cfg.device);
         hipEventDestroy(g->summed);
@@ -330,6 +346,14 @@ void shard_of(uint64_t n, int32_t rank, int32_t n_ranks, uint64_t* b, uint64_t* 
     *b = (uint64_t)(nn * (uint64_t)rank / (uint64_t)n_ranks);
     *e = (uint64_t)(nn * (uint64_t)(rank + 1) / (uint64_t)n_ranks);
 }
+
+// Rank r of G convolves the block pairs [r*P/G, (r+1)*P/G) of a file's P = ceil(floor(n/sr) / 2) pairs
+// of one-second blocks (convoluteFromAudioBuffer's blocks, kernels.cu:404-430, two per FFT pair).
+void conv_pairs_of(int32_t sample_rate, uint64_t n_frames, int32_t rank, int32_t n_ranks, uint64_t* b, uint64_t* e) {
+    const uint64_t sr = sample_rate > 0 ? (uint64_t)sample_rate : 1;
+    const uint64_t S = n_frames / sr;
+    shard_of((S + 1) / 2, rank, n_ranks, b, e);
+}
 }  // namespace
 
 extern "C" {
@@ -426,6 +450,20 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
                 ARX_HIP(hipMemsetAsync(g->d_recv[i], 0xFF, bins * sizeof(long long), r->stream));
             }
         }
+        // the all-reduce's own window on every member's stream (arx_group_allreduce_times)
+        const bool timed = render_ms != nullptr || g->members[0]->timing;
+        if (timed) {
+            if (g->ar.size() != g->members.size()) g->ar.resize(g->members.size());
+            for (size_t i = 0; i < g->members.size(); ++i) {
+                arx_renderer* r = g->members[i];
+                arx_group::ArEvents& ev = g->ar[i];
+                const int k = (int)(ev.n % arx_group::kRing);
+                ARX_HIP(hipSetDevice(r->cfg.device));
+                if (!ev.e0[k]) ARX_HIP(hipEventCreateWithFlags(&ev.e0[k], hipEventDisableSystemFence));
+                if (!ev.e1[k]) ARX_HIP(hipEventCreateWithFlags(&ev.e1[k], hipEventDisableSystemFence));
+                ARX_HIP(hipEventRecord(ev.e0[k], r->stream));
+            }
+        }
         ARX_NCCL(ncclGroupStart());
         for (size_t i = 0; i < g->members.size(); ++i) {
             arx_renderer* r = g->members[i];
@@ -438,6 +476,14 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         }
         ARX_NCCL(ncclGroupEnd());
         ++g->n_coll[0];
+        if (timed)
+            for (size_t i = 0; i < g->members.size(); ++i) {
+                arx_renderer* r = g->members[i];
+                arx_group::ArEvents& ev = g->ar[i];
+                ARX_HIP(hipSetDevice(r->cfg.device));
+                ARX_HIP(hipEventRecord(ev.e1[(int)(ev.n % arx_group::kRing)], r->stream));
+                ++ev.n;
+            }
         if (g->out_of_place)  // the sum back into the histogram the finalise reads, before the next frame's
             for (size_t i = 0; i < g->members.size(); ++i) {  // all-reduce may write the receive buffer
                 arx_renderer* r = g->members[i];
@@ -486,6 +532,61 @@ arx_status arx_group_render(arx_group* g, double* render_ms) {
         *render_ms = worst;
     }
     return ARX_OK;
+}
+
+arx_status arx_group_allreduce_times(arx_group* g, int32_t member, double* ms, size_t n, size_t* n_out) {
+    if (!g || member < 0 || member >= (int32_t)g->members.size() || (n > 0 && !ms))
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (n_out) *n_out = 0;
+    if ((size_t)member >= g->ar.size()) return ARX_OK;  // no timed all-reduce yet
+    const arx_group::ArEvents& ev = g->ar[(size_t)member];
+    ARX_HIP(hipSetDevice(g->members[(size_t)member]->cfg.device));
+    const uint64_t k = std::min<uint64_t>(std::min<uint64_t>(ev.n, (uint64_t)arx_group::kRing), (uint64_t)n);
+    for (uint64_t i = 0; i < k; ++i) {  // oldest of the last k first
+        const int slot = (int)((ev.n - k + i) % arx_group::kRing);
+        ARX_HIP(hipEventSynchronize(ev.e1[slot]));
+        float f = 0.f;
+        ARX_HIP(hipEventElapsedTime(&f, ev.e0[slot], ev.e1[slot]));
+        ms[i] = f;
+    }
+    if (n_out) *n_out = (size_t)k;
+    return ARX_OK;
+}
+
+void arx_group_conv_shard(int32_t sample_rate, uint64_t n_frames, int32_t rank, int32_t n_ranks, uint64_t* begin,
+                          uint64_t* end) {
+    uint64_t pb = 0, pe = 0;
+    conv_pairs_of(sample_rate, n_frames, rank, n_ranks, &pb, &pe);
+    const uint64_t sr = sample_rate > 0 ? (uint64_t)sample_rate : 1;
+    const uint64_t S = n_frames / sr, P = (S + 1) / 2;
+    if (P == 0) {  // nothing convolved: rank 0 owns the (zero) output
+        *begin = rank == 0 ? 0 : n_frames;
+        *end = n_frames;
+        return;
+    }
+    *begin = pb == 0 ? 0 : std::min<uint64_t>(2 * pb * sr, n_frames);
+    *end = pe == P ? n_frames : std::min<uint64_t>(2 * pe * sr, n_frames);
+    if (pe == pb) *begin = *end;
+}
+
+arx_status arx_group_convolute_device(arx_group* g, const float* const* d_in, size_t n_frames,
+                                      float* const* d_out_left, float* const* d_out_right) {
+    if (!g || g->members.empty() || !d_in || !d_out_left || !d_out_right)
+        return fail(ARX_ERR_INVALID_ARGUMENT, "bad arguments");
+    for (size_t i = 0; i < g->members.size(); ++i) {
+        arx_renderer* r = g->members[i];
+        uint64_t pb = 0, pe = 0;
+        conv_pairs_of(r->cfg.sample_rate, n_frames, g->rank0 + (int32_t)i, g->n_ranks, &pb, &pe);
+        const arx_status st = convolute_pairs(r, d_in[i], n_frames, d_out_left[i], d_out_right[i], (int64_t)pb,
+                                              (int64_t)pe);
+        if (st != ARX_OK) return st;
+    }
+    return ARX_OK;
+}
+
+int32_t arx_group_conv_sharded(arx_group* g) {
+    if (!g || g->members.empty()) return -1;
+    return conv_shards(g->members[0]) ? 1 : 0;
 }
 
 arx_status arx_group_synchronize(arx_group* g) {

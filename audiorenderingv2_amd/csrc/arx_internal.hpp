@@ -28,9 +28,10 @@ arx_status fail(arx_status s, const char* fmt, ...) __attribute__((format(printf
                                "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__);   \
     } while (0)
 
-// device counters: [0] queries [1] receiver hits [2] misses [3] error flag [4..5] counting builds
-// [6] receiver refit left the quantization grid [7] unused; the trace launch's ray-pool cursor
-// lives after them (kCursor, reset by each launch itself)
+// device counters (per frame set, cleared by each frame): [0] queries [1] receiver hits [2] misses
+// [3] error flag [4..5] counting builds [6..7] unused; the trace launch's ray-pool cursor lives after
+// them (kCursor, reset by each launch itself).  The tree's off-grid flag is NOT among them: it is
+// written by the tree updates that run before a frame's clear (arx_renderer::d_tree_flag).
 constexpr int kCounters = 8;
 constexpr int kCursor = 8;
 // receivers up to this many triangles (and whose refit fits one workgroup's LDS: 9 floats per
@@ -103,6 +104,12 @@ arx_status fif_wait_reduced(arx_renderer* r);
 arx_status fif_done_reduced(arx_renderer* r);
 // Both frame sets' streams synchronised.
 arx_status sync_renderer(arx_renderer* r);
+// arx_convolute_device restricted to the file's one-second block pairs [pair_begin, pair_end)
+// (conv_run_pairs; the group's time-block shards).
+arx_status convolute_pairs(arx_renderer* r, const float* d_in, size_t n_frames, float* d_out_left, float* d_out_right,
+                           int64_t pair_begin, int64_t pair_end);
+// Whether the renderer's file convolution plan convolves a shard on its own (conv_plan_shards).
+bool conv_shards(arx_renderer* r);
 }  // namespace arx
 
 // One renderer = one device (AudioRenderer, AudioRenderer.h:16-152).
@@ -179,6 +186,15 @@ struct arx_renderer {
     float* d_ir = nullptr;                 // 2*ir_len: L then R
     unsigned long long* d_counters = nullptr;
     unsigned long long* h_counters = nullptr;  // pinned
+    // The tree's off-grid flag (a receiver refit or re-quantization put a box outside the quantization
+    // grid; its quantized copy then falls back to whole-axis boxes): one word per renderer, outside the
+    // per-frame counters the direction pre-pass clears.  Each tree write (ensure_device_scene) runs with
+    // a new generation tree_gen and raises the word to it (atomic max) on failure, so the flag reports
+    // the tree as last written -- no clear launch, and a later clean write retires an old failure.
+    unsigned int* d_tree_flag = nullptr;
+    unsigned int* h_tree_flag = nullptr;  // pinned
+    uint32_t tree_gen = 0;
+    float debug_refit_pad = 0.0f;  // arx_debug_set_refit_pad: the refit kernel's box padding (0 = automatic)
 
     uint64_t ir_generation = 0;  // bumped whenever the IR changes (finalize_ir, set_ir): streams re-transform
     arx::ConvPlan* conv_live = nullptr;  // mic path plan (block = live block length)

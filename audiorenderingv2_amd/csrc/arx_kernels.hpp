@@ -51,7 +51,8 @@ struct RefitArgs {
     TriRec* tris;               // outputs
     BvhNode* cnodes;
     QNode2* qnodes;             // null: the quantized copy is not maintained (receiver off the grid)
-    unsigned int* flag;         // set if a box fell off the grid (never, given the host's bound)
+    unsigned int* flag;         // raised to flag_value if a box fell off the grid (never, given the host's bound)
+    unsigned int flag_value;    // the tree write's generation (arx_renderer::tree_gen)
     // CW4 copy (null wbuf: not maintained): the receiver's CW4 nodes (11 ints each: the BVH2
     // (ref, count) of the 4 slots, meta, base, self unit), its leaf triangles ((unit, local index)
     // pairs) and the top node (unit 0: child 0 = the scene root, unit 2; child 1 = the receiver
@@ -68,13 +69,13 @@ size_t receiver_refit_lds(int32_t n_tris, int32_t n_nodes, int32_t n_levels);  /
 hipError_t launch_receiver_refit(const RefitArgs& a, hipStream_t s);
 // The quantized copy of nodes [0, n) re-made on the device from the coded f32 nodes for grid g
 // (quantize_nodes16's arithmetic, bit for bit): a new scene or a grown grid costs one launch and
-// no host work or upload.  flag is set if a box falls off the grid.
+// no host work or upload.  *flag is raised to flag_value (atomic max) if a box falls off the grid.
 hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
-                            hipStream_t s);
+                            unsigned int flag_value, hipStream_t s);
 // The CW4 nodes of n f32 node records (W4NodeF: top node, scene, host-built receiver) quantized for
 // grid g into the CW4 buffer at their own units (quantize_w4, arx_wide.hpp).
 hipError_t launch_requant_w4(const W4NodeF* nodes, uint64_t n, const QGrid& g, uint4* wbuf, unsigned int* flag,
-                             hipStream_t s);
+                             unsigned int flag_value, hipStream_t s);
 
 // ---- convolution (arx_conv.hip) ----
 struct ConvPlan;  // opaque, defined in arx_conv.hip
@@ -87,6 +88,14 @@ hipError_t conv_set_ir(ConvPlan* p, const float* d_ir_left, const float* d_ir_ri
 // the audio's own column pass); with NULLs the spectra of the last conv_set_ir are used.
 hipError_t conv_run(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
                     const float* d_ir_left, const float* d_ir_right, hipStream_t s);
+// A time-block shard of conv_run: the one-second block pairs [pair_begin, pair_end) of the file
+// (clamped), writing the output frames those pairs own (arx_group_conv_shard) -- bit-identical to the
+// same frames of conv_run.  Plans without the chained pass C (conv_plan_shards false) convolve and
+// write the whole file.
+hipError_t conv_run_pairs(ConvPlan* p, const float* d_in, int64_t n_frames, float* d_out_left, float* d_out_right,
+                          const float* d_ir_left, const float* d_ir_right, int64_t pair_begin, int64_t pair_end,
+                          hipStream_t s);
+bool conv_plan_shards(const ConvPlan* p);
 const char* conv_plan_describe(const ConvPlan* p);
 // Input reuse: conv_prepare_input transforms a file's blocks once (kept in the plan until the next
 // conv_run or conv_prepare_input); conv_run_prepared convolves them with the current IR (new spectra
@@ -101,6 +110,8 @@ int64_t conv_prepared_frames(const ConvPlan* p);
 // L/R into 2*ir_len doubles (AudioRenderer.cpp:593-651, kernels.cu:345-377, 450-487).
 hipError_t conv_run_live(ConvPlan* p, const double* d_in, int64_t n_in, double* d_out_interleaved, hipStream_t s);
 int32_t conv_plan_block(const ConvPlan* p);
+// identity of the convolution kernels in this build (build.py conv_source_id; arx_conv_kernel_id)
+uint64_t conv_kernel_source_id();
 
 // ---- streaming convolution (arx_conv.hip): uniformly partitioned overlap-save, f64 ----
 struct StreamPlan;  // opaque

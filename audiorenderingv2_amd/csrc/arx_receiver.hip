@@ -61,7 +61,7 @@ __device__ void write_child(const RefitArgs& a, const double* inv, int32_t node,
     for (int k = 0; k < 3; ++k) {
         uint32_t w = 1u;  // empty: the slab between planes 0 and 1 (quantize_nodes16)
         if (!empty && !quantize_axis(a.grid, inv, k, lo[k] - a.pad, hi[k] + a.pad, w)) {
-            atomicOr(a.flag, 1u);  // off the grid: the host's bound should have prevented it
+            atomicMax(a.flag, a.flag_value);  // off the grid: the host's bound should have prevented it
             w = 0u | (65535u << 16);
         }
         q.q[k] = w;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
             }
         }
         QNode4C q;
-        if (!quantize_w4(n, a.grid, q)) atomicOr(a.flag, 1u);
+        if (!quantize_w4(n, a.grid, q)) atomicMax(a.flag, a.flag_value);
         a.wbuf[n.self] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
         a.wbuf[n.self + 1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
     }
@@ -246,19 +246,20 @@ __global__ __launch_bounds__(kRefitThreads) void receiver_refit_kernel(RefitArgs
             n.hi[2][k] = n.hi[3][k] = 0.0f;
         }
         QNode4C q;
-        if (!quantize_w4(n, a.grid, q)) atomicOr(a.flag, 1u);
+        if (!quantize_w4(n, a.grid, q)) atomicMax(a.flag, a.flag_value);
         a.wbuf[0] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
         a.wbuf[1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
     }
 }
 
 __global__ __launch_bounds__(256) void requant_w4_kernel(const W4NodeF* __restrict__ nodes, uint64_t n, QGrid g,
-                                                          uint4* __restrict__ wbuf, unsigned int* flag) {
+                                                          uint4* __restrict__ wbuf, unsigned int* flag,
+                                                          unsigned int flag_value) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const W4NodeF nd = nodes[i];
     QNode4C q;
-    if (!quantize_w4(nd, g, q)) atomicOr(flag, 1u);
+    if (!quantize_w4(nd, g, q)) atomicMax(flag, flag_value);
     wbuf[nd.self] = make_uint4(q.w[0], q.w[1], q.w[2], q.w[3]);
     wbuf[nd.self + 1] = make_uint4(q.w[4], q.w[5], q.w[6], q.w[7]);
 }
@@ -293,7 +294,8 @@ __device__ __forceinline__ bool requant_child(const QGrid& g, const float* xy, c
 }
 
 __global__ __launch_bounds__(256) void requant16_kernel(const BvhNode* __restrict__ coded, uint64_t n, QGrid g,
-                                                         QNode2* __restrict__ out, unsigned int* flag) {
+                                                         QNode2* __restrict__ out, unsigned int* flag,
+                                                         unsigned int flag_value) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const BvhNode b = coded[i];
@@ -301,26 +303,28 @@ __global__ __launch_bounds__(256) void requant16_kernel(const BvhNode* __restric
     const bool ok0 = requant_child(g, b.a, b.c, b.d[0], q.c[0]);
     const bool ok1 = requant_child(g, b.b, b.c + 2, b.d[1], q.c[1]);
     out[i] = q;
-    if (!(ok0 && ok1)) atomicOr(flag, 1u);
+    if (!(ok0 && ok1)) atomicMax(flag, flag_value);
 }
 
 }  // namespace
 
 hipError_t launch_requant_w4(const W4NodeF* nodes, uint64_t n, const QGrid& g, uint4* wbuf, unsigned int* flag,
-                             hipStream_t s) {
+                             unsigned int flag_value, hipStream_t s) {
     (void)hipGetLastError();
     if (n == 0) return hipSuccess;
     if (!nodes || !wbuf || !flag) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(requant_w4_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, g, wbuf, flag);
+    hipLaunchKernelGGL(requant_w4_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, g, wbuf, flag,
+                       flag_value);
     return hipGetLastError();
 }
 
 hipError_t launch_requant16(const BvhNode* coded, uint64_t n, const QGrid& g, QNode2* out, unsigned int* flag,
-                            hipStream_t s) {
+                            unsigned int flag_value, hipStream_t s) {
     (void)hipGetLastError();
     if (n == 0) return hipSuccess;
     if (!coded || !out || !flag) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(requant16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, coded, n, g, out, flag);
+    hipLaunchKernelGGL(requant16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, coded, n, g, out, flag,
+                       flag_value);
     return hipGetLastError();
 }
 

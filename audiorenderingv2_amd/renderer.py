@@ -521,6 +521,38 @@ class RenderGroup:
                                             {"sum": 0, "max": 1}[op]))
         return v
 
+    def allreduce_times(self, n: int = 64, member: int = 0) -> np.ndarray:
+        """Device ms of member `member`'s last min(n, 256) timed histogram all-reduces, oldest first
+        (arx_group_allreduce_times; recorded while the members' timing is on)."""
+        out = np.zeros(n, np.float64)
+        k = C.c_size_t()
+        check(lib().arx_group_allreduce_times(self._g, int(member), out.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                              C.byref(k)))
+        return out[:k.value]
+
+    def convolute_device(self, d_in, n_frames: int, d_out_left, d_out_right) -> None:
+        """Time-block sharded file convolution (arx_group_convolute_device): per local member i, the
+        whole file at d_in[i] and full-length outputs d_out_left[i] / d_out_right[i] on its device; rank
+        g writes the output frames conv_shard(g) owns."""
+        k = len(self.members)
+        P = C.c_void_p * k
+        check(lib().arx_group_convolute_device(self._g, P(*d_in), int(n_frames), P(*d_out_left), P(*d_out_right)))
+
+    def conv_shard(self, n_frames: int, rank: int, n_ranks: int | None = None) -> tuple[int, int]:
+        """Output frames [begin, end) rank `rank` owns in a sharded convolution (arx_group_conv_shard)."""
+        b, e = C.c_uint64(), C.c_uint64()
+        lib().arx_group_conv_shard(int(self.settings.sample_rate), int(n_frames), int(rank),
+                                   int(self.n_ranks if n_ranks is None else n_ranks), C.byref(b), C.byref(e))
+        return int(b.value), int(e.value)
+
+    @property
+    def conv_sharded(self) -> bool:
+        """Whether the convolution plan shards by time blocks (else every rank convolves the whole file)."""
+        v = int(lib().arx_group_conv_sharded(self._g))
+        if v < 0:
+            check(6)
+        return v == 1
+
     def debug_force_collectives(self, on: bool = True, out_of_place: bool = False) -> None:
         """Tests only (arx_debug_group_force_collectives): every collective issued at one rank too,
         out of place into 0xFF-filled receive buffers if asked."""

@@ -8,7 +8,9 @@ One step = one pass of the hot path on every GPU (BASELINE.json configs[2], per 
   trace this GPU's 1M-ray shard x 16 bounces (fused HIP kernel) -> one RCCL all-reduce (int64
   SUM) of the 2 x 96000-bin histogram -> finalize the stereo f32 IR (libarx's native group API,
   arx_group_render) -> IR spectra + file-mode FFT convolution of A_Clapper_Board.wav channel 0
-  (807 498 frames, 48 kHz) on every GPU.
+  (807 498 frames, 48 kHz), time-block sharded over the GPUs (arx_group_convolute_device: each GPU
+  convolves its share of the file's one-second block pairs; the union is the one-GPU output bit for
+  bit, no collective).
 
 How the N GPUs are driven (plan_ranks):
   * plain `python bench.py --gpus N`: ONE process drives N GPUs through one native group
@@ -22,8 +24,9 @@ libarx (arx_device_alloc, the renderer's own stream and per-launch event rings),
 the /opt/rocm HIP / RCCL runtime it was built and tested against (`runtime` in the JSON line).
 Asking for more GPUs than the box has fails loudly instead of printing a smaller line.
 Inputs are resident in HBM before timing.  Rank 0 prints ONE JSON line.
-Scaling is weak: every GPU owns 1M rays of an N*1M-ray launch (energy normalised by the total
-count, devicePrograms.cu:208) and convolves its own copy of the stream.
+Scaling is weak for the rays: every GPU owns 1M rays of an N*1M-ray launch (energy normalised by
+the total count, devicePrograms.cu:208); the file's convolution is shared (strong) and counted once.
+A watchdog ends a run whose steps stop completing with one {"status": "hang", ...} line (exit 3).
 """
 from __future__ import annotations
 
@@ -33,8 +36,10 @@ import hashlib
 import json
 import math
 import os
+import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 import numpy as np
@@ -72,7 +77,12 @@ def bytes_per_bounce(n_tris: int) -> int:
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
 NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2", 2: "4-wide compressed (CW4)"}  # arx_stats.trace_format
 PROFILES = "r05"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
-CONV_TRAFFIC = "r04/conv_traffic_r04j.json"  # the full convolution's PMC traffic (its kernels are unchanged since)
+# the C3 file convolution's PMC traffic (tools/gpu_conv_pmc.sh), guarded by arx_conv_kernel_id
+CONV_TRAFFIC = "r06/conv_traffic.json"
+# the GPU box's full-launch parity record of C3 (tests/test_gpu_full_launch.py with ARX_PARITY_RECORD),
+# guarded by tree hash and trace kernel identity
+FULL_LAUNCH_PARITY = "r06/full_launch_parity/c3_whole_launch.json"
+HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md: measured-achievable HBM read bandwidth
 
 
 # ----------------------------------------------------------------------------- rank plumbing ---
@@ -157,6 +167,63 @@ class Ranks:
         return float(self.g.allreduce([v], "sum")[0]) if self.multi else float(v)
 
 
+class Watchdog:
+    """A step that never completes (a cross-GPU ordering bug in the frames-in-flight all-reduce chain,
+    a collective some rank skipped) must not leave the driver's run hung without a line: a daemon
+    thread watches the time since the last progress beat and, past the armed limit, prints ONE JSON
+    line {"status": "hang", "phase", "rank", ...} and ends the process (exit code 3; no re-exec, no
+    retry).  The main thread's GPU waits are ctypes calls, which release the GIL, so the thread runs
+    while they block."""
+
+    def __init__(self, rank: int, world: int, out=None, on_hang=None, poll_s: float = 0.5):
+        self.rank, self.world = rank, world
+        self.out = out if out is not None else sys.stdout
+        self.on_hang = on_hang if on_hang is not None else os._exit
+        self.limit_s = None
+        self.phase = "setup"
+        self.steps_done = 0
+        self.info = {}
+        self.fired = False
+        self._last = time.monotonic()
+        self._lock = threading.Lock()
+        self._poll = poll_s
+        threading.Thread(target=self._run, name="bench-watchdog", daemon=True).start()
+
+    def arm(self, limit_s: float, phase: str | None = None) -> None:
+        with self._lock:
+            self.limit_s = float(limit_s)
+            self._last = time.monotonic()
+            if phase:
+                self.phase = phase
+
+    def disarm(self) -> None:
+        with self._lock:
+            self.limit_s = None
+
+    def beat(self, phase: str | None = None, step: bool = False) -> None:
+        with self._lock:
+            self._last = time.monotonic()
+            if phase:
+                self.phase = phase
+            if step:
+                self.steps_done += 1
+
+    def _run(self) -> None:
+        while not self.fired:
+            time.sleep(self._poll)
+            with self._lock:
+                if self.limit_s is None or time.monotonic() - self._last <= self.limit_s:
+                    continue
+                self.fired = True
+                line = {"status": "hang", "metric": METRIC, "phase": self.phase, "rank": self.rank,
+                        "world": self.world, "steps_done": self.steps_done,
+                        "seconds_since_progress": round(time.monotonic() - self._last, 2),
+                        "limit_s": self.limit_s, **self.info}
+            self.out.write(json.dumps(line) + "\n")
+            self.out.flush()
+            self.on_hang(3)
+
+
 # ------------------------------------------------------------------------------ CPU baseline ---
 def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> dict:
     """The CPU oracle (naive C ray loop + median-split BVH) on this host, bounded samples of the
@@ -164,6 +231,8 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> d
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as po
     from audiorenderingv2_amd.renderer import place_receiver_vertices
+
+    build_note = native_oracle(po)
     from audiorenderingv2_amd.scene import CONFERENCE_EMITTER, CONFERENCE_LISTENER
 
     L, R = receiver
@@ -200,7 +269,7 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> d
     dtc = time.perf_counter() - t1
     return {
         "value": allc, "unit": "ray-bounces/s", "cores": cores, "kind": "port",
-        "sample": f"oracle/arx_oracle.c (-O3, median-split BVH): rays 0..{n2} of the same launch on {cores} "
+        "sample": f"oracle/arx_oracle.c ({build_note}, median-split BVH): rays 0..{n2} of the same launch on {cores} "
                   f"threads = the CPUs this process may use (affinity capped by the cgroup quota) ({d2:.1f} s); "
                   f"1 thread: rays 0..{n1} ({d1:.1f} s)",
         "single_thread_value": one,
@@ -208,6 +277,22 @@ def cpu_baseline(scene, receiver, wl, n_total_rays, audio, budget_s: float) -> d
         "convolution_sample": f"f64 oracle block convolution, 1 thread, {x.size} frames x 2 ears",
         "cpu_model": _cpu_model(),
     }
+
+
+def native_oracle(po) -> str:
+    """Build the oracle with -O3 -march=native for THIS host (`make -C oracle native` into
+    a temporary directory, a few seconds) and load it; the portable liboracle.so if that fails."""
+    out = os.path.join(tempfile.mkdtemp(prefix="arx_oracle_native_"), "liboracle_native.so")
+    try:
+        r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "native", f"NATIVE_OUT={out}"],
+                           capture_output=True, text=True, timeout=180)
+        if r.returncode == 0 and os.path.exists(out):
+            po.use_library(out)
+            return "-O3 -march=native -ffp-contract=off, built on this host"
+        why = (r.stderr or r.stdout).strip().splitlines()[-1:] or ["make failed"]
+    except (OSError, subprocess.SubprocessError, RuntimeError) as e:
+        why = [str(e)]
+    return f"-O3 portable liboracle.so (the -march=native build failed: {why[0][:120]})"
 
 
 def available_cores() -> int:
@@ -239,7 +324,7 @@ def _cpu_model() -> str:
 C5 = dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000)  # configs[4]: 1M rays x 16 per frame in total
 
 
-def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int) -> dict:
+def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int, wd: "Watchdog | None" = None) -> dict:
     """SURVEY.md §8d C5 (configs[4]): 1M rays x 16 bounces per frame in total, sharded over the job's
     GPUs (125K per GPU on 8), the listener moving 0.05 m/frame along +x with yaw += 1 deg/frame.
     Frame latency = host wall time of: receiver re-placement (receiver sub-tree only, no scene
@@ -262,13 +347,26 @@ def moving_listener(g, ranks: Ranks, frames: int, rays_per_gpu: int) -> dict:
         g.synchronize()
         if k >= 3:  # first frames warm the receiver rebuild path
             lat.append((time.perf_counter() - t0) * 1e3)
+        if wd is not None:
+            wd.beat()
     a = np.array(lat)
-    return {"frames": frames, "rays_per_frame": int(np.prod(C5["rays"])), "rays_per_gpu": rays_per_gpu,
-            "gpus": g.n_ranks, "p50_ms": ranks.max(float(np.percentile(a, 50))),
-            "p99_ms": ranks.max(float(np.percentile(a, 99))), "max_ms": ranks.max(float(a.max())),
-            "budget_ms": 1000.0 / 60.0, "walk_m": 0.05 * (frames + 2),
-            "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + RCCL all-reduce (N > 1) + finalize + "
-                         "IR spectra, on a C5 group of its own (1M rays x 16 per frame over all GPUs)"}
+    out = {"frames": frames, "rays_per_frame": int(np.prod(C5["rays"])), "rays_per_gpu": rays_per_gpu,
+           "gpus": g.n_ranks, "p50_ms": ranks.max(float(np.percentile(a, 50))),
+           "p99_ms": ranks.max(float(np.percentile(a, 99))), "max_ms": ranks.max(float(a.max())),
+           "budget_ms": 1000.0 / 60.0, "walk_m": 0.05 * (frames + 2),
+           "per_frame": "listener re-place (+0.05 m x, +1 deg yaw) + trace + RCCL all-reduce (N > 1) + finalize + "
+                        "IR spectra, on a C5 group of its own (1M rays x 16 per frame over all GPUs)"}
+    # the frames' all-reduces, measured (HIP events around the collective on each member's stream;
+    # recorded when the group times its launches, at N > 1 or with the collectives forced)
+    n_ar = min(frames, 256)  # the group's all-reduce event ring: the last 256 frames
+    ars = [g.allreduce_times(n_ar, i) for i in range(len(g.members))]
+    if n_ar > 0 and all(len(x) == n_ar for x in ars):
+        worst = np.max(np.stack(ars), axis=0)
+        out["allreduce_p50_ms"] = ranks.max(float(np.percentile(worst, 50)))
+        out["allreduce_p99_ms"] = ranks.max(float(np.percentile(worst, 99)))
+        out["allreduce_source"] = (f"measured: arx_group_allreduce_times over the last {n_ar} frames, slowest member "
+                                   "per frame, max over ranks")
+    return out
 
 
 def allreduce_model_us(n_ranks: int, nbytes: int, alpha_us: float = 3.0, link_gbs: float = 153.0) -> float:
@@ -375,6 +473,19 @@ def profile_guard(prof: dict | None, workload: str, stats: dict,
     return prof, "matches " + " / ".join(keys)
 
 
+def conv_profile_guard(prof: dict | None, workload: str) -> tuple[dict | None, str]:
+    """The stored convolution traffic applies only to the C3 workload and to the convolution kernels
+    it was taken of (arx_conv_kernel_id, a hash of arx_conv.hip compiled into libarx)."""
+    from audiorenderingv2_amd._lib import lib
+    if prof is None:
+        return None, "missing"
+    want = {"workload": workload, "conv_kernel_id": f"{int(lib().arx_conv_kernel_id()):016x}"}
+    bad = [k for k, v in want.items() if prof.get(k) != v]
+    if bad:
+        return None, "stale: " + ", ".join(f"{k} {prof.get(k)!r} != {want[k]!r}" for k in bad)
+    return prof, "matches workload / conv_kernel_id"
+
+
 @contextlib.contextmanager
 def _stdout_to_stderr():
     """Send whatever native libraries write on fd 1 to fd 2 for the duration."""
@@ -409,10 +520,20 @@ def main(argv=None) -> int:
     ap.add_argument("--frames-in-flight", type=int, choices=(1, 2, 3), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
-                         "too.  Default at every N (so the 1..8-GPU lines compare like with like): 3 for c2, 2 for "
-                         "c3, 1 for c4 (its 48 ms launches lose 5 %% to the overlap).  Each frame's all-reduce runs "
-                         "on its own frame stream after the previous frame's (tests/test_gpu_collectives.py runs "
-                         "that chain with every collective forced on one GPU)")
+                         "too.  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 48 ms launches lose 5 %% to "
+                         "the overlap).  Default at N > 1: 1, until a multi-GPU run of the frames-in-flight "
+                         "all-reduce chain is on record (each frame's all-reduce runs on its own frame stream after "
+                         "the previous frame's; tests/test_gpu_collectives.py runs that chain with every "
+                         "collective forced on one GPU only)")
+    ap.add_argument("--replicated-convolution", action="store_true",
+                    help="every GPU convolves the whole file (replicas) instead of its time-block shard "
+                         "(arx_group_convolute_device); the convolved-frames rates then count every copy")
+    ap.add_argument("--watchdog-s", type=float, default=None,
+                    help="no progress for this long -> one JSON line {\"status\": \"hang\", ...} and exit 3 "
+                         "(default: 180 s through the pre-roll, then max(30 s, 50 x the pre-roll step))")
+    ap.add_argument("--debug-hang-at-step", type=int, default=-1,
+                    help="tests only: stall the host inside timed step K (a stand-in for a GPU wait that never "
+                         "returns), so the watchdog fires")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="no-op: the two-group pipelined leg (round 3) became --frames-in-flight")
     ap.add_argument("--timing-events", action="store_true",
@@ -448,6 +569,7 @@ def main(argv=None) -> int:
         raise SystemExit(f"bench.py: --gpus {args.gpus} needs {plan['local_gpus_needed']} visible GPU(s) in this "
                          f"process, the HIP runtime sees {have}; refusing to print a line for fewer GPUs")
     world, rank = plan["world"], plan["rank"]
+    wd = Watchdog(rank, world)
     wl = WORKLOADS[args.workload]
     rx, ry, rz = wl["rays"]
     if wl.get("total"):  # a fixed total split over the GPUs (strong scaling)
@@ -494,39 +616,61 @@ def main(argv=None) -> int:
     for m in members:
         d = m.settings.device
         bufs.append((DeviceBuffer.from_numpy(d, audio_np), DeviceBuffer(d, 4 * frames), DeviceBuffer(d, 4 * frames)))
+    # the convolution: each rank convolves its time-block shard of the file (arx_group_convolute_device;
+    # the union is the one-GPU convolution bit for bit, tests/test_gpu_group_conv.py), or with
+    # --replicated-convolution the whole file on every GPU
+    sharded_conv = not args.replicated_convolution
+    d_in, d_ol, d_or = [b[0].ptr for b in bufs], [b[1].ptr for b in bufs], [b[2].ptr for b in bufs]
+    conv_plan_shards = g.conv_sharded
+    own = [g.conv_shard(frames, rank + i) for i in range(len(members))]
+    unique_frames = frames if (sharded_conv or world == 1) else world * frames
 
     # timing: the renderers' own HIP events around each trace launch and each convolution (on
     # their streams); no further markers in the timed loop -- each costs the stream a few us
     def step():
         g.render(timed=False)  # clear + trace + RCCL all-reduce + finalize, every GPU
-        for m, (x, ol, orr) in zip(members, bufs):
-            m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
+        if sharded_conv:
+            g.convolute_device(d_in, frames, d_ol, d_or)
+        else:
+            for m, (x, ol, orr) in zip(members, bufs):
+                m.convolute_device(x.ptr, frames, ol.ptr, orr.ptr)
+        wd.beat(step=True)
+
+    def sync(phase=None):
+        g.synchronize()
+        wd.beat(phase)
 
     if args.frames_in_flight is None:
-        args.frames_in_flight = wl["fif"]
+        args.frames_in_flight = wl["fif"] if world == 1 else 1
+    wd.info["frames_in_flight"] = args.frames_in_flight
     g.set_frames_in_flight(args.frames_in_flight)
     # pre-roll: untimed steps until the GPU runs at its sustained clock, then the contract's W warmup
     # steps.  The ranks agree after every step whether to go on (max over ranks), so each takes the
     # same number of steps and their all-reduces stay paired.
+    wd.arm(args.watchdog_s or 180.0, "preroll")
     t_pre, pre_steps = time.perf_counter(), 0
     while True:
         step()
-        g.synchronize()
+        sync()
         pre_steps += 1
         if ranks.max(1.0 if time.perf_counter() - t_pre < args.preroll_s else 0.0) == 0.0:
             break
     preroll_s = time.perf_counter() - t_pre
+    wd_limit = args.watchdog_s or max(30.0, 50.0 * preroll_s / pre_steps)
+    wd.arm(wd_limit, "warmup")
     for _ in range(args.warmup):
         step()
-    g.synchronize()
+    sync()
     g.stats()
     setup_s = time.perf_counter() - t_setup
     ranks.barrier()
-    g.synchronize()
+    sync("timed")
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        if k == args.debug_hang_at_step:
+            time.sleep(2.0 * wd_limit + 5.0)  # tests only: the watchdog ends the process first
         step()
-    g.synchronize()
+    sync()
     ranks.barrier()
     t1 = time.perf_counter()
     elapsed = ranks.max(t1 - t0)
@@ -543,15 +687,16 @@ def main(argv=None) -> int:
     # a single-frame leg: the same group, W + K steps with one frame in flight.
     single_frame = None
     if args.frames_in_flight > 1:
+        wd.beat("single_frame")
         g.set_frames_in_flight(1)
         for _ in range(args.warmup):
             step()
-        g.synchronize()
+        sync()
         ranks.barrier()
         t0s = time.perf_counter()
         for _ in range(args.steps):
             step()
-        g.synchronize()
+        sync()
         ranks.barrier()
         el1 = ranks.max(time.perf_counter() - t0s)
         q1 = int(round(ranks.sum(int(g.stats()["queries"]))))
@@ -561,27 +706,41 @@ def main(argv=None) -> int:
     # The per-launch kernel times: W + K more single-frame steps with the timing events on (HIP
     # events on the renderer's stream around the direction pre-pass + trace kernel, and around the IR
     # spectra + convolution), the K timed launches of GPU 0 of this process.
+    wd.beat("kernel_times")
     g.set_frames_in_flight(1)
     g.set_timing(True)
     for _ in range(args.warmup):
         step()
-    g.synchronize()
+    sync()
     ranks.barrier()
     t0k = time.perf_counter()
     for _ in range(args.steps):
         step()
-    g.synchronize()
+    sync()
     ranks.barrier()
     timed_leg_ms = ranks.max(time.perf_counter() - t0k) / args.steps * 1e3
     trace_list = m0.trace_times(args.steps)
     assert len(trace_list) == args.steps, (len(trace_list), args.steps)
     trace_ms = float(np.mean(trace_list))
+    # the histogram all-reduce's own window (HIP events on each member's stream around the RCCL call,
+    # arx_group_allreduce_times), the slowest member, max over ranks; none at one rank unless forced
+    ar_lists = [g.allreduce_times(args.steps, i) for i in range(len(members))]
+    if all(len(a) == args.steps for a in ar_lists):
+        allreduce_ms = ranks.max(max(float(np.mean(a)) for a in ar_lists))
+        allreduce_why = (f"RCCL int64 all-reduce of 2 x {ir_len} bins over {world} rank(s): HIP events around the "
+                         "collective on each member's stream (arx_group_allreduce_times), mean of the K timed "
+                         "launches, slowest member, max over ranks")
+    else:
+        allreduce_ms = None
+        allreduce_why = "one rank: arx_group_render skips the no-op all-reduce (--debug-force-collectives times it)"
     conv_ms_all = []
     for m in members:
         cl = m.conv_times(args.steps)
         assert len(cl) == args.steps, (len(cl), args.steps)
         conv_ms_all.append(float(np.mean(cl)))
     conv_ms = conv_ms_all[0]
+    # the frames rank 0's convolution window covers: its shard, or the whole file
+    conv_frames_rank0 = (own[0][1] - own[0][0]) if (sharded_conv and conv_plan_shards and world > 1) else frames
     conv_ms_max = ranks.max(max(conv_ms_all))
     # Input reuse (arx_convolute_prepare_input / _prepared): the reference re-convolves the same file
     # with every new IR (full_render_cycle, AudioRenderer.cpp:790-798), so the file's blocks can be
@@ -589,6 +748,7 @@ def main(argv=None) -> int:
     # with the convolution of the prepared input, its kernel window beside the full one.
     reuse = None
     if not args.no_reuse:
+        wd.beat("input_reuse")
         g.set_frames_in_flight(1)
         for m, (x, _, _) in zip(members, bufs):
             m.convolute_prepare_input(x.ptr, frames)
@@ -600,12 +760,13 @@ def main(argv=None) -> int:
 
         for _ in range(args.warmup):
             step_reuse()
-        g.synchronize()
+        sync()
         ranks.barrier()
         t0r = time.perf_counter()
         for _ in range(args.steps):
             step_reuse()
-        g.synchronize()
+            wd.beat()
+        sync()
         ranks.barrier()
         elr = ranks.max(time.perf_counter() - t0r)
         reuse_ms = float(np.mean(m0.conv_times(args.steps)))
@@ -621,6 +782,7 @@ def main(argv=None) -> int:
     # the audio in host memory and both output channels back in host memory (AudioRenderer.cpp:663-750).
     host_leg = None
     if not args.no_host_leg:
+        wd.beat("host_buffers")
         g.set_frames_in_flight(1)
 
         def step_host():
@@ -629,13 +791,14 @@ def main(argv=None) -> int:
 
         for _ in range(args.warmup):
             step_host()
-        g.synchronize()
+        sync()
         ranks.barrier()
         t0h = time.perf_counter()
         host_conv = []
         for _ in range(args.steps):
             host_conv.append(max(step_host()))
-        g.synchronize()
+            wd.beat()
+        sync()
         ranks.barrier()
         elh = ranks.max(time.perf_counter() - t0h)
         host_leg = {"ms_per_step": elh / args.steps * 1e3,
@@ -664,8 +827,10 @@ def main(argv=None) -> int:
             g5.set_receiver_model(*receiver)
             g5.set_scene(scene)
         g5.setEmitterPosInOptix(CONFERENCE_EMITTER)
-        g5.set_timing(False)  # host wall clock per frame; no event markers in it
-        moving = moving_listener(g5, ranks, args.c5_frames, int(np.prod(C5["rays"])) // world)
+        # host wall clock per frame; event markers only where there is an all-reduce to time
+        g5.set_timing(world > 1 or args.debug_force_collectives)
+        wd.beat("moving_listener")
+        moving = moving_listener(g5, ranks, args.c5_frames, int(np.prod(C5["rays"])) // world, wd)
         g5.close()
     bpb = bytes_per_bounce(n_tris)
     achieved = q_m0 * bpb / (trace_ms * 1e-3) / 1e9
@@ -674,9 +839,13 @@ def main(argv=None) -> int:
                                        ("workload", "tree_hash", "trace_kernel_id"))
     td, td_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_td_c3.json")), args.workload, st0)
     vmem, vmem_why = profile_guard(load_profile(os.path.join(PROFILES, "trace_vmem_ceiling.json")), args.workload, st0)
-    conv_traffic = load_profile(CONV_TRAFFIC)
-    conv_frames_s = world * frames / (conv_ms_max * 1e-3)  # the convolution kernels' own window
-    conv_frames_step = world * frames * args.steps / elapsed  # the pipeline: frames convolved per timed step
+    conv_traffic, conv_traffic_why = conv_profile_guard(load_profile(CONV_TRAFFIC), args.workload)
+    parity, parity_why = profile_guard(load_profile(FULL_LAUNCH_PARITY), args.workload, st0,
+                                       ("workload", "tree_hash", "trace_kernel_id"))
+    # unique stereo frames: the file once per step when it is time-block sharded (or on one GPU), every
+    # GPU's copy with --replicated-convolution
+    conv_frames_s = unique_frames / (conv_ms_max * 1e-3)  # the convolution kernels' own window
+    conv_frames_step = unique_frames * args.steps / elapsed  # the pipeline: frames convolved per timed step
     result = {
         "metric": METRIC,
         "value": value,
@@ -698,7 +867,15 @@ def main(argv=None) -> int:
             "max_bounces": wl["max_bounces"],
             "sample_rate": wl["sample_rate"],
             "ir_len": ir_len,
-            "audio_frames_per_gpu": frames,
+            "audio_frames": frames,
+            "convolution": ("one GPU: the whole file" if world == 1 else
+                            (f"time-block sharded over {world} GPUs (arx_group_convolute_device): rank r owns the "
+                             f"output frames of block pairs [r P/{world}, (r+1) P/{world}) and re-makes its seam pair, "
+                             "no collective" if conv_plan_shards else
+                             "this plan has no chained pass: every GPU convolves the whole file")
+                            if sharded_conv else f"replicas: each of the {world} GPUs convolves the whole file"),
+            "convolved_frames_per_step": unique_frames,
+            "conv_frames_owned_rank0": [int(own[0][0]), int(own[0][1])],
             "frames_in_flight": args.frames_in_flight,
             "parallelism": (f"ray-shard x{world}, "
                             + ("native RCCL int64 IR all-reduce per step" if world > 1 else
@@ -731,11 +908,14 @@ def main(argv=None) -> int:
         "convolved_frames_per_s": conv_frames_step,
         "convolved_frames_per_s_kernel_window": conv_frames_s,
         "convolved_frames_per_s_labels": {
-            "convolved_frames_per_s": "whole job, per timed step: stereo frames convolved (every GPU's copy of the "
-                                      "file) x K / the K steps' wall time, trace included",
+            "convolved_frames_per_s": "whole job, per timed step: unique stereo frames convolved "
+                                      "(config.convolved_frames_per_step: the file once when sharded or on one GPU, "
+                                      "every copy with --replicated-convolution) x K / the K steps' wall time, trace "
+                                      "included",
             "convolved_frames_per_s_kernel_window": "the same frames / the slowest GPU's IR-spectra + convolution "
                                                     "window alone (the renderer's HIP events, arx_conv_times)"},
-        "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms},
+        "phases_ms_rank0": {"trace_kernel": trace_ms, "ir_spectra_and_convolution": conv_ms, "allreduce": allreduce_ms},
+        "phases_allreduce_why": allreduce_why,
         "convolution_input_reuse": reuse,
         "host_buffers": host_leg,
         "trace_kernel_build": {"vgprs": int(st0["trace_vgprs"]), "waves_per_simd": int(st0["trace_waves_per_simd"]),
@@ -744,7 +924,20 @@ def main(argv=None) -> int:
                                "tree_hash": f"{int(st0['tree_hash']):016x}"},
         "roofline": {
             "kernel": "trace_kernel",
-            "bound": "hbm",
+            # what binds the kernel (PMC: the vector-memory return path TD, VALU beside it); achieved /
+            # peak / frac below are the contract's HBM byte convention, whose tree bytes
+            # are L1 / L2 hits, so frac can pass what HBM can deliver
+            "bound": "td",
+            "convention_bound": "hbm",
+            "convention_exceeds_achievable_hbm": achieved > HBM_ACHIEVABLE_GBS,
+            "achievable_hbm_GBps": HBM_ACHIEVABLE_GBS,
+            "queries_match_oracle_full_launch": (
+                bool(parity["queries_gpu"] == parity["queries_oracle"] and parity["ir_left_bit_exact"]
+                     and parity["ir_right_bit_exact"] and parity["queries_gpu"] == q_m0)
+                if parity and world == 1 else None),
+            "queries_oracle_full_launch": parity["queries_oracle"] if parity else None,
+            "full_launch_parity_source": f"profiles/{FULL_LAUNCH_PARITY} (tests/test_gpu_full_launch.py on the GPU box: "
+                                         "the oracle traced every ray of the launch): " + parity_why,
             "convention": "SURVEY.md §8d algorithmic bytes per ray-bounce (32 + 32 + 64 ceil(log2 T) + 48); the "
                           "tree is cache-resident, so this is a byte convention, not the binding unit: the "
                           "kernel is co-limited by the vector-memory return path and VALU issue (roofline_td, "
@@ -769,15 +962,17 @@ def main(argv=None) -> int:
         },
         "roofline_convolution": {
             "bound": "hbm",
-            "achieved": frames * BYTES_PER_STEREO_FRAME / (conv_ms * 1e-3) / 1e9,
+            "achieved": conv_frames_rank0 * BYTES_PER_STEREO_FRAME / (conv_ms * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": frames * BYTES_PER_STEREO_FRAME / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac": conv_frames_rank0 * BYTES_PER_STEREO_FRAME / (conv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frames_rank0": conv_frames_rank0,
             "algorithmic_bytes_per_stereo_frame": BYTES_PER_STEREO_FRAME,
-            "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and args.workload == "c3" else None,
-            "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and args.workload == "c3" else None,
+            "traffic": conv_traffic["total_bytes_per_step"] if conv_traffic and world == 1 else None,
+            "traffic_over_algorithmic": conv_traffic["ratio"] if conv_traffic and world == 1 else None,
             "traffic_source": f"profiles/{CONV_TRAFFIC} (tools/gpu_conv_pmc.sh: rocprofv3 --pmc "
-                              "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra)",
+                              "FETCH_SIZE x2 + WRITE_SIZE per pass, the C3 convolution incl. IR spectra, one GPU): "
+                              + conv_traffic_why,
         },
     }
     if vmem and counts:
@@ -836,6 +1031,7 @@ def main(argv=None) -> int:
                                                                              int(np.prod(C5["rays"])) // 8)
     if rank == 0 and not args.no_streaming and wl["sample_rate"] == 48000:
         result["streaming"] = streaming_leg(m0, audio_np, 4096)
+    wd.disarm()  # the CPU baseline below runs no GPU work
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(scene, receiver, wl, total_rays, audio_np, args.cpu_baseline_seconds)
     if rank == 0:

@@ -170,6 +170,9 @@ arx_status arx_attach_histogram(arx_renderer* r, int64_t* d_hist, size_t n_elems
 arx_status arx_finalize_ir(arx_renderer* r);
 arx_status arx_ir_device(arx_renderer* r, float** d_left, float** d_right, size_t* ir_len);
 arx_status arx_copy_ir(arx_renderer* r, float* h_left, float* h_right, size_t ir_len);
+/* Counters of the last frame (synchronises the renderer's stream).  ARX_ERR_INTERNAL (stats still
+ * filled in) when the tree as last written has a box off the 16-bit quantization grid (receiver refit
+ * or device re-quantization; never with the host's grid bounds). */
 arx_status arx_get_stats(arx_renderer* r, arx_stats* out);
 /* Device times (HIP events on the renderer's stream) of the last min(n, arx_timing_ring()) trace launches, oldest
  * first, into ms[0..*n_out); synchronises on them.  The reference's timed window (Time taken by
@@ -196,6 +199,9 @@ arx_status arx_set_timing(arx_renderer* r, int32_t on);
  * count, and bench.py uses a stored profile only when all three match its own run.  No
  * reference counterpart (measurement plumbing). */
 uint64_t arx_trace_kernel_id(void);
+/* The same for the file convolution's kernels (build.py conv_source_id): the guard of the stored
+ * convolution traffic profile (profiles/<round>/conv_traffic.json). */
+uint64_t arx_conv_kernel_id(void);
 /* Replace the renderer's IR with caller data (host, ir_len floats per ear), e.g. a stored or
  * measured IR; the next convolution uses it.  No reference equivalent (its IR only comes
  * from render()). */
@@ -268,8 +274,36 @@ arx_status arx_group_render(arx_group* g, double* render_ms);
  * frames, in and out of place, bit-identical to a plain renderer); its first multi-GPU run is the
  * 8-GPU bench, which keeps the one-GPU frames-in-flight policy at every N. */
 arx_status arx_group_set_frames_in_flight(arx_group* g, int32_t n);
-/* arx_set_timing on every member. */
+/* arx_set_timing on every member; with it on (or render_ms asked for), arx_group_render also puts HIP
+ * events around each member's histogram all-reduce. */
 arx_status arx_group_set_timing(arx_group* g, int32_t on);
+/* Device times of member `member`'s last min(n, 256) timed histogram all-reduces (the RCCL collective's
+ * window on that member's stream, queueing behind the member's own trace excluded), oldest first;
+ * synchronises on them.  *n_out = 0 when no all-reduce was timed (a one-rank group skips its no-op
+ * all-reduce unless arx_debug_group_force_collectives). */
+arx_status arx_group_allreduce_times(arx_group* g, int32_t member, double* ms, size_t n, size_t* n_out);
+
+/* Time-block sharded file convolution ("time blocks sharded ... only the n - sr overlap
+ * is summed at shard seams"; the reference convolves on one GPU, kernels.cu:404-430).  The file's
+ * floor(n/sr) one-second blocks form P = ceil(blocks / 2) FFT pairs; rank g of G convolves the pairs
+ * [g*P/G, (g+1)*P/G) with its member's IR and writes the output frames they own,
+ * arx_group_conv_shard's [begin, end), into its member's full-length buffers d_out_left[i] /
+ * d_out_right[i] (n_frames floats each, on member i's device; d_in[i] there holds the whole file).
+ * The seam -- the tail of the block before a shard -- is re-made by the shard itself from that block's
+ * input, not received from the neighbour, so the data path has no collective; the union of the ranks'
+ * frames is arx_convolute_device's output bit for bit.  Plans without the chained pass
+ * (arx_group_conv_sharded == 0: ir_len != 2 sr, or an IR length without a direct mixed-radix split)
+ * convolve and write the whole file on every rank.  Asynchronous on the members' streams, like
+ * arx_convolute_device; arx_conv_times per member time each shard. */
+arx_status arx_group_convolute_device(arx_group* g, const float* const* d_in, size_t n_frames,
+                                      float* const* d_out_left, float* const* d_out_right);
+/* The output frames [begin, end) rank `rank` of n_ranks owns in a sharded convolution of n_frames at
+ * sample_rate (host only; ranges of the ranks tile [0, n_frames)). */
+void arx_group_conv_shard(int32_t sample_rate, uint64_t n_frames, int32_t rank, int32_t n_ranks, uint64_t* begin,
+                          uint64_t* end);
+/* 1 if the group's convolution plan shards (see arx_group_convolute_device), 0 if every rank convolves
+ * the whole file, -1 on error. */
+int32_t arx_group_conv_sharded(arx_group* g);
 arx_status arx_group_synchronize(arx_group* g);
 arx_status arx_group_copy_ir(arx_group* g, float* h_left, float* h_right, size_t ir_len); /* member 0 */
 /* Queries / receiver hits / misses summed over this process's members; times = the longest. */
@@ -291,7 +325,9 @@ arx_status arx_convolute_device(arx_renderer* r, const float* d_in, size_t n_fra
 /* Input reuse for the reference's re-render pattern: full_render_cycle (AudioRenderer.cpp:790-798,
  * called by main.cpp:40-67 on every listener move) convolves the SAME file with every new IR.
  * arx_convolute_prepare_input transforms the file's one-second blocks once (device input, n_frames
- * samples; the input buffer may be reused by the caller afterwards); arx_convolute_prepared then
+ * samples).  The transform is queued on the renderer's stream, not run by the call: the caller may
+ * overwrite d_in only once that stream has finished it (after arx_get_stats, arx_copy_ir or a
+ * synchronisation of the stream, or from work ordered after it on that stream); arx_convolute_prepared then
  * convolves them with the renderer's current IR into the caller's device outputs (n_frames each,
  * *n_frames set when non-NULL) -- bit-identical to arx_convolute_device on the same input, without
  * the input's forward transform.  The prepared input stays until the next arx_convolute_device /
@@ -386,6 +422,16 @@ arx_status arx_debug_wide_stats(const float* tri_vertices, const float* tri_abso
 arx_status arx_debug_trace_profile(arx_renderer* r, uint64_t* out, size_t n_words, size_t* n_out);
 /* Raw device counters of the last trace (n <= 8): [0] queries [1] receiver hits [2] misses. */
 arx_status arx_debug_trace_counters(arx_renderer* r, uint64_t* out, size_t n);
+/* Host only: the tree-size guard every scene passes (arx_set_scene, arx_group_set_scene): the trace
+ * kernel addresses nodes (64 B) and triangle records (48 B) with 31-bit buffer offsets, so n_nodes * 64
+ * and n_tris * 48 must stay <= 2^31 - 1 (ARX_ERR_INVALID_ARGUMENT beyond).  The 28-bit triangle index
+ * of a leaf code (~(index * 16 + count)) is wider than that limit needs. */
+arx_status arx_debug_check_tree_limits(uint64_t n_nodes, uint64_t n_tris);
+/* Tests only: the receiver refit kernel's box padding (0 = automatic, the builder's pad).  A pad far
+ * beyond the quantization grid's margin makes the refit raise the tree's off-grid flag (its quantized
+ * boxes then fall back to whole-axis, still conservative), which arx_get_stats reports as
+ * ARX_ERR_INTERNAL until a later tree write (a listener move, a new scene) is clean again. */
+arx_status arx_debug_set_refit_pad(arx_renderer* r, float pad);
 /* Force the trace kernel's other paths (parity tests of the paths real scenes rarely take): the
  * default is the 16-bit quantized BVH2 with the LDS stack; bit 0 = the f32 coded BVH2 (taken
  * automatically while the emitter is off the quantization grid), bit 1 = the global-memory

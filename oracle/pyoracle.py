@@ -47,6 +47,15 @@ class OrcStream(C.Structure):
                 ("blocks", C.c_int64), ("hist", C.c_void_p), ("X", C.c_void_p), ("G", C.c_void_p)]
 
 
+def use_library(path: str) -> None:
+    """Load this build of the oracle instead of liboracle.so (bench.py's -march=native CPU baseline);
+    must precede the first call into the oracle."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("the oracle library is already loaded")
+    LIB_PATH = path
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
@@ -55,8 +64,8 @@ def build() -> str:
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or (
-                os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "arx_oracle.c"))):
+        if LIB_PATH == os.path.join(HERE, "liboracle.so") and (not os.path.exists(LIB_PATH) or (
+                os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "arx_oracle.c")))):
             build()
         L = C.CDLL(LIB_PATH)
         F = C.POINTER(C.c_float)

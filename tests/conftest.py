@@ -29,6 +29,22 @@ def world_scene(scene, listener, yaw=0.0):
     return tv, ta
 
 
+def oracle_threads() -> int:
+    """Threads for the CPU oracle: the CPUs this process may run on, capped by a cgroup CPU quota (the
+    GPU box's affinity mask lists the whole machine while its share is 16 CPUs)."""
+    import math
+
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 64))
+
+
 @pytest.fixture(scope="session")
 def c1_scene():
     from audiorenderingv2_amd.scene import reference_config_materials, test_obj_scene

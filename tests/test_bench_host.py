@@ -127,3 +127,27 @@ def test_ranks_issue_collectives_only_across_processes_unless_forced():
         r.max(1.0)
         r.sum(1.0)
         assert [op for _, op in g.calls] == ["sum", "max", "sum"]
+
+
+def test_watchdog_fires_once_without_progress_and_not_while_beating():
+    import io
+    import json
+    import time
+
+    out, codes = io.StringIO(), []
+    wd = bench.Watchdog(2, 8, out=out, on_hang=codes.append, poll_s=0.05)
+    wd.info["frames_in_flight"] = 1
+    wd.arm(0.4, "timed")
+    for _ in range(12):  # beats keep it quiet
+        time.sleep(0.1)
+        wd.beat(step=True)
+    assert codes == [] and out.getvalue() == ""
+    wd.disarm()
+    time.sleep(0.6)  # disarmed: quiet
+    assert codes == []
+    wd.arm(0.2, "moving_listener")
+    time.sleep(0.8)
+    assert codes == [3]
+    d = json.loads(out.getvalue())
+    assert d["status"] == "hang" and d["phase"] == "moving_listener" and d["rank"] == 2 and d["world"] == 8
+    assert d["steps_done"] == 12 and d["frames_in_flight"] == 1 and d["seconds_since_progress"] >= 0.2

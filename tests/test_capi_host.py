@@ -176,3 +176,23 @@ def test_main_style_caller_compiles_against_reference_glm(tmp_path):
     subprocess.run([gxx, "-std=c++17", "-O1", "-Wall", "-Werror", "-DARX_DEMO_GLM", "-I", glm, "-I",
                     os.path.join(REPO, "include"), os.path.join(REPO, "tests", "cpp", "main_style_demo.cpp"),
                     "-L", pkg, "-larx", f"-Wl,-rpath,{pkg}", "-o", str(tmp_path / "main_style_demo")], check=True)
+
+
+def test_tree_limits_guard_the_kernels_offsets_and_leaf_codes():
+    """check_buffer_offsets (arx_debug_check_tree_limits) admits a tree up to the trace kernel's 31-bit
+    buffer offsets and rejects one node / one triangle record beyond; at that limit the largest leaf
+    code ~(index * 16 + count) and the largest inner-node code (its index) still fit int32, and stay
+    clear of the empty-child code -- so the code width never binds before the offsets do."""
+    from audiorenderingv2_amd._lib import ARX_OK, lib
+
+    max_off = 0x7FFFFFFF
+    tris_max, nodes_max = max_off // 48, max_off // 64
+    L = lib()
+    assert L.arx_debug_check_tree_limits(1, tris_max) == ARX_OK
+    assert L.arx_debug_check_tree_limits(nodes_max, 1) == ARX_OK
+    assert L.arx_debug_check_tree_limits(1, tris_max + 1) == 1  # ARX_ERR_INVALID_ARGUMENT
+    assert L.arx_debug_check_tree_limits(nodes_max + 1, 1) == 1
+    assert "31-bit buffer offsets" in L.arx_last_error().decode()
+    last_leaf = (tris_max - 1) * 16 + 15  # the leaf code's positive form (count <= 15)
+    assert last_leaf <= 0x7FFFFFFF and (nodes_max - 1) <= 0x7FFFFFFF
+    assert ~last_leaf != ~16 and last_leaf != 16  # kEmptyChildCode = ~16 (a leaf of 0 triangles)

@@ -46,10 +46,19 @@ def test_bench_prints_one_contract_line():
     # both convolution rates, labelled: per timed step (trace included) and the kernels' own window
     cf, ck = d["convolved_frames_per_s"], d["convolved_frames_per_s_kernel_window"]
     assert set(d["convolved_frames_per_s_labels"]) == {"convolved_frames_per_s", "convolved_frames_per_s_kernel_window"}
-    frames = d["config"]["audio_frames_per_gpu"]
+    frames = d["config"]["audio_frames"]
+    assert d["config"]["convolved_frames_per_step"] == frames  # one GPU: the file once
+    assert d["config"]["conv_frames_owned_rank0"] == [0, frames]
     assert abs(cf - frames * d["steps"] / (d["ms_per_step"] * 1e-3 * d["steps"])) < 1e-6 * cf
     assert abs(ck - frames / (d["phases_ms_rank0"]["ir_spectra_and_convolution"] * 1e-3)) < 1e-6 * ck
     assert ck > cf
+    # what binds the trace kernel, beside the HBM byte convention; the oracle's full-launch record is
+    # C3's (null on this c2 line), the all-reduce phase null at one rank with its reason
+    assert rf["bound"] == "td" and rf["convention_bound"] == "hbm"
+    assert rf["convention_exceeds_achievable_hbm"] == (rf["achieved"] > rf["achievable_hbm_GBps"])
+    assert "queries_match_oracle_full_launch" in rf and "full_launch_parity_source" in rf
+    assert d["phases_ms_rank0"]["allreduce"] is None and "one rank" in d["phases_allreduce_why"]
+    assert "march=native" in d["cpu_baseline"]["sample"], d["cpu_baseline"]["sample"]
     # one GPU: the group's no-op all-reduce is skipped, and the line says so
     assert "skips its no-op IR all-reduce" in d["config"]["parallelism"]
     # the one-GPU projection of an 8-GPU rank's C5 frame reports its all-reduce as a model only
@@ -100,3 +109,32 @@ def test_bench_rank_path_under_torchrun():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and "ncclCommInitRank" in d["config"]["parallelism"] and d["value"] > 0
+
+
+def test_bench_watchdog_ends_a_hung_step_with_one_line():
+    """A step that never completes must not hang the driver's run: the watchdog prints one
+    {"status": "hang", ...} line and exits 3 (here through the test-only host stall in step 1)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "c2", "--steps", "3", "--warmup", "1",
+           "--c5-frames", "0", "--no-cpu-baseline", "--no-streaming", "--watchdog-s", "4", "--debug-hang-at-step", "1"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[:2000]
+    d = json.loads(lines[0])
+    assert d["status"] == "hang" and d["phase"] == "timed" and d["rank"] == 0 and d["world"] == 1
+    assert d["limit_s"] == 4.0 and d["seconds_since_progress"] > 4.0 and d["frames_in_flight"] == 3
+
+
+def test_bench_forced_collectives_time_the_allreduce():
+    """With the collectives forced at one rank, the line carries the measured all-reduce phase and
+    the C5 leg's measured all-reduce percentiles."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "c2", "--steps", "3", "--warmup", "1",
+           "--c5-frames", "5", "--no-cpu-baseline", "--no-streaming", "--no-reuse", "--no-host-leg",
+           "--debug-force-collectives"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    ar = d["phases_ms_rank0"]["allreduce"]
+    assert ar is not None and 0 < ar < 50, d["phases_allreduce_why"]
+    ml = d["moving_listener"]
+    assert ml["allreduce_p50_ms"] > 0 and "measured" in ml["allreduce_source"]
