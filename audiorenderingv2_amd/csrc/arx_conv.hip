@@ -1773,7 +1773,8 @@ hipError_t conv_run_pairs(ConvPlan* p, const float* d_in, int64_t n_frames, floa
     if (n_frames <= 0) return hipSuccess;
     p->prepared = false;  // any other file convolution discards a prepared input (pass A overwrites its spectra)
     int64_t S = n_frames / p->sr;  // kernels.cu:413
-    if (S == 0) {  // nothing convolved: the reference output stays zero
+    if (S == 0) {  // nothing convolved: the reference output stays zero (a shard past pair 0 owns none of it)
+        if (pair_begin > 0) return hipSuccess;
         hipError_t e = hipMemsetAsync(d_out_left, 0, (size_t)n_frames * sizeof(float), s);
         if (e == hipSuccess) e = hipMemsetAsync(d_out_right, 0, (size_t)n_frames * sizeof(float), s);
         return e;

@@ -352,6 +352,11 @@ void shard_of(uint64_t n, int32_t rank, int32_t n_ranks, uint64_t* b, uint64_t* 
 void conv_pairs_of(int32_t sample_rate, uint64_t n_frames, int32_t rank, int32_t n_ranks, uint64_t* b, uint64_t* e) {
     const uint64_t sr = sample_rate > 0 ? (uint64_t)sample_rate : 1;
     const uint64_t S = n_frames / sr;
+    if (S == 0) {  // no block: rank 0 writes the (zero) output, the others nothing (conv_run_pairs)
+        *b = rank == 0 ? 0 : 1;
+        *e = 1;
+        return;
+    }
     shard_of((S + 1) / 2, rank, n_ranks, b, e);
 }
 }  // namespace

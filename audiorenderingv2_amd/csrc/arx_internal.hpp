@@ -29,7 +29,7 @@ arx_status fail(arx_status s, const char* fmt, ...) __attribute__((format(printf
     } while (0)
 
 // device counters (per frame set, cleared by each frame): [0] queries [1] receiver hits [2] misses
-// [3] error flag [4..5] counting builds [6..7] unused; the trace launch's ray-pool cursor lives after
+// [3] error flag [4..7] counting builds (node steps, triangle tests, leader-node steps, step slots); the trace launch's ray-pool cursor lives after
 // them (kCursor, reset by each launch itself).  The tree's off-grid flag is NOT among them: it is
 // written by the tree updates that run before a frame's clear (arx_renderer::d_tree_flag).
 constexpr int kCounters = 8;

@@ -802,6 +802,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     uint32_t n_q = 0, n_rx = 0, n_miss = 0;
 #if ARX_TRACE_COUNT  // measurement builds only (build.py --exp ... -D ARX_TRACE_COUNT=1)
     uint32_t n_steps = 0, n_tris = 0;
+    // the scalar-fetch probe: node lane-steps whose node is the wave leader's (the first lane with a
+    // node to step), and node-step slots the wave ran -- a scalar load of the leader's node could
+    // serve the former without vector-memory (TD) work
+    uint32_t n_leader = 0, n_slots = 0;
 #endif
 #if ARX_TRACE_PROF  // measurement builds only: wave-uniform tallies (popcounts of ballots)
     // [0] start [1] end [2] rays [3] queries [4] node-step slots run [5] node lane-steps [6] leaf
@@ -930,6 +934,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                         pf[5] += __popcll(mk);
                     }
 #endif
+#if ARX_TRACE_COUNT
+                    {
+                        const unsigned long long ml = __ballot(t.node >= 0);
+                        if (ml) {
+                            const int lead = __shfl(t.node, (int)__builtin_ctzll(ml), 64);
+                            n_leader += (t.node >= 0 && t.node == lead) ? 1u : 0u;
+                            n_slots += (lane & 63) == 0 ? 1u : 0u;
+                        }
+                    }
+#endif
                     if (t.node >= 0) {
 #if ARX_TRACE_COUNT
                         ++n_steps;
@@ -965,9 +979,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     }
 #endif
     flush_counters(a, n_q, n_rx, n_miss, lane);
-#if ARX_TRACE_COUNT  // [4] node steps, [5] leaf triangle tests (lane level)
+#if ARX_TRACE_COUNT  // [4] node steps, [5] leaf triangle tests (lane level), [6] leader-node lane-steps, [7] step slots
     atomicAdd(a.counters + 4, (unsigned long long)n_steps);
     atomicAdd(a.counters + 5, (unsigned long long)n_tris);
+    atomicAdd(a.counters + 6, (unsigned long long)n_leader);
+    atomicAdd(a.counters + 7, (unsigned long long)n_slots);
 #endif
 }
 
