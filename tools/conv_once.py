@@ -8,9 +8,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch  # noqa: E402
-
-from audiorenderingv2_amd import AudioRenderer, RenderSettings  # noqa: E402
+from audiorenderingv2_amd import AudioRenderer, DeviceBuffer, RenderSettings  # noqa: E402
 from audiorenderingv2_amd.scene import reference_audio  # noqa: E402
 from audiorenderingv2_amd._lib import use_library  # noqa: E402
 
@@ -28,14 +26,15 @@ for _ in range(2):
     ir = np.zeros(2 * sr, np.float32)
     ir[rng.integers(0, 2 * sr, 20000)] = rng.exponential(1e-4, 20000).astype(np.float32)
     irs.append(ir)
-dx = torch.from_numpy(x).cuda()
-dl, dr = torch.empty_like(dx), torch.empty_like(dx)
+# device buffers of libarx itself (no second GPU framework in the process)
+dx = DeviceBuffer.from_numpy(0, x)
+dl, dr = DeviceBuffer(0, x.nbytes), DeviceBuffer(0, x.nbytes)
 ms = []
 for _ in range(n):
     r.set_ir(*irs)
-    r.convolute_device(dx.data_ptr(), x.size, dl.data_ptr(), dr.data_ptr())
-    torch.cuda.synchronize()
+    r.convolute_device(dx.ptr, x.size, dl.ptr, dr.ptr)
+    r.stats()  # synchronises the renderer's stream
     ms.append(r.conv_times(1)[0])
 print(f"frames {x.size} conv {np.median(ms[1:] if n > 1 else ms) * 1e3:.1f} us (median of {max(n - 1, 1)}) "
-      f"checksum {float(dl.double().abs().sum() + dr.double().abs().sum()):.9e} "
+      f"checksum {float(np.abs(dl.to_numpy(np.float32).astype(np.float64)).sum() + np.abs(dr.to_numpy(np.float32).astype(np.float64)).sum()):.9e} "
       f"lib {os.path.basename(os.environ.get('ARX_LIB', 'libarx.so'))}", flush=True)

@@ -29,4 +29,13 @@ frames = 807498
 out["total_bytes_per_step"] = total
 out["algorithmic_bytes_per_step"] = 52 * frames
 out["ratio"] = total / (52 * frames)
+# the guard bench.py checks (bench.conv_profile_guard): workload and the convolution kernels' identity
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from audiorenderingv2_amd._lib import lib  # noqa: E402
+
+out["workload"] = "c3"
+out["conv_kernel_id"] = f"{int(lib().arx_conv_kernel_id()):016x}"
+out["method"] = ("tools/gpu_conv_pmc.sh: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 128-B requests tallied at 64 B) and "
+                 "WRITE_SIZE in separate passes, per pass of the C3 convolution (tools/conv_once.py, IR spectra "
+                 "included)")
 print(json.dumps(out, indent=1))
