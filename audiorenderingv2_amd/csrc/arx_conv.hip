@@ -1133,7 +1133,10 @@ __global__ __launch_bounds__(512) void pass_b_mr(MrArgs m) {
 // LDS: 2 x N2 per wave (S's spectrum; G's row, then the product), W_N2 (N2).
 // XS (input reuse, conv_run_prepared): the S rows already hold the block pairs' row spectra (pass_b_mr
 // mode 3), so only the G rows are transformed forward.
-template <bool R7, int LM, int L2, bool XS>
+// HONLY (the IR spectra alone, conv_set_ir): no block pair -- the G rows are transformed and H_L / H_R
+// stored, by the same arithmetic as the fused pass's, so the spectra a convolution uses are the same
+// bits whichever call made them.
+template <bool R7, int LM, int L2, bool XS, bool HONLY = false>
 __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     constexpr int IT = LM / 64;
     extern __shared__ __attribute__((aligned(16))) double2 lds[];
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     double2* gbuf = spec + N2;
     double2* gmir = self ? gbuf : lds + (size_t)(w ^ 1) * 2 * N2 + N2;
     double2* tw2 = lds + (size_t)4 * N2;
-    double2* row = a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
+    double2* row = HONLY ? nullptr : a.S + (size_t)batch * 3 * a.M + (int64_t)k1 * N2;
     double2 v[IT], g[IT], twq[IT], twr[IT];
     const int step = 64 * k1, dq = step / N2, dr = step - dq * N2;
     int q = (j * k1) / N2, r = j * k1 - q * N2;
@@ -1162,7 +1165,7 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     for (int it = 0; it < IT; ++it) {
         const int i = j + 64 * it;
         const bool in = live && i < N2;
-        v[it] = in ? row[i] : make_double2(0.0, 0.0);
+        v[it] = (in && !HONLY) ? row[i] : make_double2(0.0, 0.0);
         g[it] = in ? a.G[(int64_t)k1 * N2 + i] : make_double2(0.0, 0.0);
         twq[it] = in ? a.tw[(int64_t)q * N2] : make_double2(1.0, 0.0);
         twr[it] = in ? a.tw[r] : make_double2(1.0, 0.0);
@@ -1184,7 +1187,7 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
     }
     __syncthreads();
     CONV_PROF_MARK(1);
-    if constexpr (XS)
+    if constexpr (XS || HONLY)
         fft_wave_any<R7, LM, L2>(gbuf, tw2, m.f2, j, -1);
     else
         fft2_wave_any<R7, LM, L2>(spec, gbuf, tw2, m.f2, j, -1);
@@ -1212,6 +1215,7 @@ __global__ __launch_bounds__(128) void pass_b_pair(MrArgs m) {
             }
         }
     }
+    if constexpr (HONLY) return;  // no barrier below is reached by any wave
     __syncthreads();  // every mirror read is done before gbuf is overwritten
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -1582,11 +1586,12 @@ static size_t mr_lds_a(const ConvPlan* p, int tc) {
 static size_t mr_lds_c(const ConvPlan* p, int tc) { return ((size_t)tc * mr_col_stride(p->N1, tc) + p->N1) * sizeof(double2); }
 static unsigned mr_rows(const ConvPlan* p, int rows) { return (unsigned)((p->N1 + rows - 1) / rows); }
 static size_t mr_lds_b(const ConvPlan* p, int rows) { return ((size_t)rows * 2 * p->N2 + p->N2) * sizeof(double2); }
-template <bool R7, int LM, int L2, bool XS = false>
+template <bool R7, int LM, int L2, bool XS = false, bool HONLY = false>
 static void launch_b_pair(const ConvPlan* p, int batches, MrArgs m, hipStream_t s) {
     const unsigned units8 = (unsigned)((p->N1 + 1) / 2 + 7) / 8 * 8;  // see pass_b_pair's XCD mapping
     m.batches = batches;
-    hipLaunchKernelGGL((pass_b_pair<R7, LM, L2, XS>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2), s, m);
+    hipLaunchKernelGGL((pass_b_pair<R7, LM, L2, XS, HONLY>), dim3(units8 * (unsigned)batches), dim3(128), mr_lds_b(p, 2),
+                       s, m);
 }
 template <int MODE, bool R7, int LM, int L2>
 static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipStream_t s) {
@@ -1596,12 +1601,20 @@ static void launch_b_mr(const ConvPlan* p, int rows, int batches, MrArgs m, hipS
                        m);
 }
 
-// IR spectra alone (arx_prepare_ir_spectra, the live path)
+#ifndef ARX_CONV_TCA
+#define ARX_CONV_TCA 8
+#endif
+// IR spectra alone (arx_prepare_ir_spectra, the live path, a file shorter than one block): the packed
+// IR h_L + i h_R through pass A's IR batch (to G) and pass B's mirror-row split (to H) -- the route a
+// file convolution with a new IR takes, so H comes out the same bits either way
 template <bool R7, int LM, int L1, int L2>
 static void mr_ir(const ConvPlan* p, const PassArgs& a, hipStream_t s) {
     const MrArgs m = mr_args(p, a);
-    hipLaunchKernelGGL((pass_a_mr<1, R7, LM, L1>), dim3(mr_tiles(p, 2), 2), dim3(128), mr_lds_a(p, 2), s, m);
-    launch_b_mr<1, R7, LM, L2>(p, 1, 2, m, s);
+    MrArgs mi = m;
+    mi.p.n_pairs = 0;  // batch 0 of this launch is the IR (pass_a_mr mode 0's batch past the pairs)
+    hipLaunchKernelGGL((pass_a_mr<0, R7, LM, L1>), dim3(mr_tiles(p, ARX_CONV_TCA), 1u), dim3(64 * ARX_CONV_TCA),
+                       mr_lds_a(p, ARX_CONV_TCA), s, mi);
+    launch_b_pair<R7, LM, L2, false, true>(p, 1, m, s);
 }
 
 // File convolution; with_ir: the packed IR's columns ride in pass A's launch as an extra batch and

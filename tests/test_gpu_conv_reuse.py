@@ -102,3 +102,32 @@ def test_prepared_short_input_and_nothing_prepared():
         for b in [x, *out]:
             b.close()
         r.close()
+
+
+@pytest.mark.parametrize("sr", [48000, 16000, 44100])
+def test_ir_spectra_are_the_same_bits_whichever_call_made_them(sr):
+    """The IR spectra come out of one route -- the packed IR through pass A's IR batch and pass B's
+    mirror-row split -- whether a file convolution made them with its own first pass, a file shorter
+    than one block made them alone, or arx_prepare_ir_spectra did: a convolution's output does not
+    depend on the calls before it."""
+    rng = np.random.default_rng(sr)
+    n = 2 * sr
+    irl, irr = sparse_ir(n, rng), sparse_ir(n, rng)
+    x = (0.3 * rng.standard_normal(5 * sr + 321)).astype(np.float32)
+    short = rng.standard_normal(sr // 3).astype(np.float32)
+    outs = []
+    for how in ("fresh", "short_file_first", "prepared_spectra"):
+        r = AudioRenderer(RenderSettings(rays=(1, 1, 1), sample_rate=sr, ir_length_in_seconds=2))
+        r.set_ir(irl, irr)
+        if how == "short_file_first":
+            r.convoluteAudioFile(short)  # no whole block: the spectra are made alone
+        elif how == "prepared_spectra":
+            r.prepare_ir_spectra(file=True, live=False)
+        L, R, _, _ = r.convoluteAudioFile(x)
+        outs.append((L, R))
+        r.close()
+    for L, R in outs[1:]:
+        assert np.array_equal(bits(L), bits(outs[0][0])) and np.array_equal(bits(R), bits(outs[0][1]))
+    for got, ir in zip(outs[0], (irl, irr)):
+        ref = po.convolute_audio(x, sr, ir)
+        assert np.abs(got - ref).max() <= np.spacing(np.float32(np.abs(ref).max()))

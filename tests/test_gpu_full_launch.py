@@ -14,7 +14,7 @@ loop over the whole launch, devicePrograms.cu:192-254.
       10 M launch's own energy and fixed-point scale (a rank's shard on 10 GPUs)
   C5  the moving-listener walk (0.05 m / frame along +x, yaw +1 deg / frame; bench.py
       moving_listener), 600 frames of 1 M x 16 through the device receiver refit; frames 0, 300 and
-      599 against the oracle at those poses
+      599 against the oracle at those poses (the walk leaves the stand-in room at frame 100)
 
 With ARX_PARITY_RECORD=<dir> each test also writes a JSON record of what it compared (profiles/r06/
 keeps the GPU box's records; bench.py reads the C3 one, guarded by tree hash and kernel identity).
@@ -61,7 +61,7 @@ def oracle(scene, s, listener=CONFERENCE_LISTENER, yaw=0.0, begin=0, end=None):
     return irl, irr, st
 
 
-def check_same(name, gpu_ir, gst, ora_ir, ost, extra=None):
+def check_same(name, gpu_ir, gst, ora_ir, ost, extra=None, require_hits=True):
     counts_g = (int(gst["queries"]), int(gst["receiver_hits"]), int(gst["misses"]))
     counts_o = (int(ost["queries"]), int(ost["receiver_hits"]), int(ost["misses"]))
     bits = [bool(np.array_equal(g.view(np.uint32), o.view(np.uint32))) for g, o in zip(gpu_ir, ora_ir)]
@@ -77,7 +77,8 @@ def check_same(name, gpu_ir, gst, ora_ir, ost, extra=None):
             json.dump(rec, fh, indent=1)
     assert counts_g == counts_o, rec
     assert all(bits), rec
-    assert gst["receiver_hits"] > 0
+    if require_hits:
+        assert gst["receiver_hits"] > 0
     return rec
 
 
@@ -144,4 +145,7 @@ def test_c5_walk_frames(conference, c5_walk, frame):
     pose = (x0 + 0.05 * frame, y0, z0)
     ir, st = c5_walk[frame]
     irl, irr, ost = oracle(conference, C3, listener=pose, yaw=float(frame % 360))
-    check_same(f"c5_walk_frame{frame}", ir, st, (irl, irr), ost, {"pose": list(pose), "yaw": frame % 360})
+    # the walk leaves the 20 m room at frame 100 (x = 10 m): later frames see the room's outside wall
+    # and almost no receiver hits, which the oracle must reproduce just the same
+    check_same(f"c5_walk_frame{frame}", ir, st, (irl, irr), ost, {"pose": list(pose), "yaw": frame % 360},
+               require_hits=frame == 0)
