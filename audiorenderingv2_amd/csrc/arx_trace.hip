@@ -430,6 +430,12 @@ typedef int arx_i32x4 __attribute__((ext_vector_type(4)));
 // by name as composable_kernel's amd_buffer_addressing.hpp does for the raw forms)
 __device__ arx_i32x4 arx_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
                                                  int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+#ifndef ARX_TRACE_SFETCH
+#define ARX_TRACE_SFETCH 0  // design experiment: the wave leader's node by one scalar load (see node_step)
+#endif
+typedef int arx_i32x8 __attribute__((ext_vector_type(8)));
+// s_buffer_load_dwordx8 (a scalar LOAD through the scalar data cache; the descriptor as 4 SGPRs)
+__device__ arx_i32x8 arx_s_buffer_load_b256(arx_i32x4 rsrc, int offset, int aux) __asm("llvm.amdgcn.s.buffer.load.v8i32");
 __device__ __forceinline__ uint4 node_half(__amdgpu_buffer_rsrc_t rs, int node, int half) {
 #if ARX_TRACE_IDXEN
     const arx_i32x4 v = arx_struct_buffer_load_b128(rs, node, half * 16, 0, 0);
@@ -452,7 +458,8 @@ __device__ __forceinline__ uint4 node_half(__amdgpu_buffer_rsrc_t rs, int node, 
 //   f32: the coded BvhNode (56 of its 64 B), ix = inv, oix = o*inv.
 template <int FMT, typename Stack, bool PIN = true>
 __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, float oiz, Trav& t, const Stack& stk,
-                                          __amdgpu_buffer_rsrc_t rs, const uint4* __restrict__ ncache) {
+                                          __amdgpu_buffer_rsrc_t rs, const uint4* __restrict__ ncache,
+                                          arx_i32x4 qrs) {
     constexpr bool Q16 = FMT == kFmtQ16;
     // the pop candidate is read first, so its latency hides under the node fetch (slot sp - 1 is
     // not touched by this step's write to slot sp)
@@ -480,8 +487,22 @@ __device__ __forceinline__ void node_step(const Ray& r, float oix, float oiy, fl
             A = make_uint4(cached ? Al.x : Ag.x, cached ? Al.y : Ag.y, cached ? Al.z : Ag.z, cached ? Al.w : Ag.w);
             B = make_uint4(cached ? Bl.x : Bg.x, cached ? Bl.y : Bg.y, cached ? Bl.z : Bg.z, cached ? Bl.w : Bg.w);
         } else {
+#if ARX_TRACE_SFETCH
+            // the wave leader's node (the first lane stepping) by one scalar load, no vector-memory
+            // (TD) work; only the lanes at another node issue the two 16-B vector loads
+            const int lead = __builtin_amdgcn_readfirstlane(t.node);
+            const arx_i32x8 sn = arx_s_buffer_load_b256(qrs, lead * (int)sizeof(QNode2), 0);
+            if (t.node != lead) {
+                A = node_half(rs, t.node, 0);
+                B = node_half(rs, t.node, 1);
+            } else {
+                A = make_uint4((uint32_t)sn.s0, (uint32_t)sn.s1, (uint32_t)sn.s2, (uint32_t)sn.s3);
+                B = make_uint4((uint32_t)sn.s4, (uint32_t)sn.s5, (uint32_t)sn.s6, (uint32_t)sn.s7);
+            }
+#else
             A = node_half(rs, t.node, 0);
             B = node_half(rs, t.node, 1);
+#endif
         }
         na = make_float4((float)(A.x & 0xffffu), (float)(A.x >> 16), (float)(A.y & 0xffffu), (float)(A.y >> 16));
         nb = make_float4((float)(B.x & 0xffffu), (float)(B.x >> 16), (float)(B.y & 0xffffu), (float)(B.y >> 16));
@@ -785,6 +806,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
     const __amdgpu_buffer_rsrc_t nrs = W4 ? buffer_rsrc(a.wbuf)
                                           : (Q16 ? buffer_rsrc(a.qnodes, ARX_TRACE_IDXEN ? (short)sizeof(QNode2) : (short)0)
                                                  : buffer_rsrc(a.cnodes));
+    // the quantized nodes' descriptor as four scalars (the scalar-load experiment, ARX_TRACE_SFETCH)
+    arx_i32x4 qrs;
+    {
+        const unsigned long long qa = (unsigned long long)a.qnodes;
+        qrs.x = (int)(uint32_t)qa;
+        qrs.y = (int)((qa >> 32) & 0xffffu);
+        qrs.z = 0x7fffffff;
+        qrs.w = 0x00020000;
+    }
     const float4* tbase = W4 ? reinterpret_cast<const float4*>(a.wbuf) : reinterpret_cast<const float4*>(a.tris);
     const __amdgpu_buffer_rsrc_t trs = buffer_rsrc(tbase);
     const uint64_t n = a.ray_end - a.ray_begin;
@@ -949,7 +979,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void trace_kernel(TraceArgs a) {
                         ++n_steps;
 #endif
                         if constexpr (W4) node_step_w4(r, oix, oiy, oiz, t, stk, nrs);
-                        else node_step<FMT, Stack, !LEAN>(r, oix, oiy, oiz, t, stk, nrs, ncache);
+                        else node_step<FMT, Stack, !LEAN>(r, oix, oiy, oiz, t, stk, nrs, ncache, qrs);
                     }
                 }
             } else {
