@@ -99,3 +99,23 @@ def test_bench_rank_path_and_local_group_count_the_one_gpu_launch(n_gpus):
     assert "ncclCommInitAll" in local["config"]["parallelism"]
     assert ranks["scaling"] == local["scaling"] == "strong"
     assert ranks["ray_bounces_per_step"] == local["ray_bounces_per_step"] == one["ray_bounces_per_step"]
+
+
+def test_time_block_sharded_convolution_over_all_gpus(conference, n_gpus):
+    """arx_group_convolute_device over distinct GPUs: every rank convolves its block pairs of the
+    clapper file on its own device; the union of the ranks' frames is the one-GPU convolution."""
+    from test_gpu_group_conv import assemble_and_check, one_gpu_conv, sharded
+    from audiorenderingv2_amd.scene import reference_audio
+
+    x, sr = reference_audio("clapper")
+    s = RenderSettings(rays=(100, 100, 4), sample_rate=48000, base_power=3.62, max_bounces=16)
+    g = RenderGroup(s, devices=list(range(n_gpus)), scene=conference, receiver=receiver_local())
+    try:
+        g.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        g.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+        g.render()
+        assert g.conv_sharded
+        ref = one_gpu_conv(g.get_ir(), sr, x)
+        assemble_and_check(sharded(g, x), ref, x.size, whole_file=False)
+    finally:
+        g.close()
