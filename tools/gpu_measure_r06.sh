@@ -5,6 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
+mkdir -p gpurun_out/r06
 RD=r06 TAG=${TAG:-r06} bash tools/gpu_profile.sh > gpurun_out/r06/profile_${TAG:-r06}.txt 2>&1 || { tail -20 gpurun_out/r06/profile_${TAG:-r06}.txt; exit 1; }
 tail -5 gpurun_out/r06/profile_${TAG:-r06}.txt
 bash tools/gpu_conv_pmc.sh > gpurun_out/r06/conv_traffic.json 2> gpurun_out/r06/conv_pmc.err || { tail -20 gpurun_out/r06/conv_traffic.json gpurun_out/r06/conv_pmc.err; exit 1; }
