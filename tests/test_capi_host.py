@@ -196,3 +196,35 @@ def test_tree_limits_guard_the_kernels_offsets_and_leaf_codes():
     last_leaf = (tris_max - 1) * 16 + 15  # the leaf code's positive form (count <= 15)
     assert last_leaf <= 0x7FFFFFFF and (nodes_max - 1) <= 0x7FFFFFFF
     assert ~last_leaf != ~16 and last_leaf != 16  # kEmptyChildCode = ~16 (a leaf of 0 triangles)
+
+
+def test_conv_shards_tile_the_file():
+    """arx_group_conv_shard (host only): for any world size the ranks' output frames tile [0, n) in
+    rank order; a rank owns whole one-second block pairs (2 sr frames each) of the file's
+    ceil(floor(n / sr) / 2) pairs, the last rank with pairs also the tail past them; a file without a
+    whole block belongs to rank 0."""
+    import ctypes as C
+
+    from audiorenderingv2_amd._lib import lib
+
+    L = lib()
+    for sr in (16000, 48000, 1100):
+        for n in (0, 5, sr - 1, sr, 2 * sr, 2 * sr + 7, 16 * sr + 42, 807498, 17 * sr):
+            S = n // sr
+            P = (S + 1) // 2
+            for W in (1, 2, 3, 4, 7, 8, 16):
+                cursor = 0
+                for r in range(W):
+                    b, e = C.c_uint64(), C.c_uint64()
+                    L.arx_group_conv_shard(sr, n, r, W, C.byref(b), C.byref(e))
+                    b, e = b.value, e.value
+                    assert b <= e and (b == cursor or b == e), (sr, n, W, r, b, e, cursor)
+                    if e > b:
+                        pb, pe = P * r // W, P * (r + 1) // W
+                        if P == 0:
+                            assert r == 0 and (b, e) == (0, n)
+                        else:
+                            assert b == (0 if pb == 0 else 2 * pb * sr)
+                            assert e == (n if pe == P else 2 * pe * sr)
+                    cursor = max(cursor, e)
+                assert cursor == n, (sr, n, W)
