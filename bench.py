@@ -76,7 +76,7 @@ def bytes_per_bounce(n_tris: int) -> int:
 
 BYTES_PER_STEREO_FRAME = 52  # SURVEY.md §8d (reference algorithm n = 2*sr, hop = sr)
 NODE_FORMATS = {0: "f32 BVH2", 1: "16-bit quantized BVH2", 2: "4-wide compressed (CW4)"}  # arx_stats.trace_format
-PROFILES = "r05"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
+PROFILES = "r06"  # profiles/<round>/: the guarded PMC-derived profiles of the current kernel and tree
 # the C3 file convolution's PMC traffic (tools/gpu_conv_pmc.sh), guarded by arx_conv_kernel_id
 CONV_TRAFFIC = "r06/conv_traffic.json"
 # the GPU box's full-launch parity record of C3 (tests/test_gpu_full_launch.py with ARX_PARITY_RECORD),
