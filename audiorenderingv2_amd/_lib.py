@@ -182,6 +182,7 @@ SIGNATURES = {
     "arx_group_conv_shard": (None, [C.c_int32, C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_uint64)]),
     "arx_group_conv_sharded": (C.c_int32, [_P]),
+    "arx_group_convolute_audio_file": (C.c_int, [_P, _F, C.c_size_t, _F, _F, _D, _D]),
     "arx_group_synchronize": (C.c_int, [_P]),
     "arx_group_copy_ir": (C.c_int, [_P, _F, _F, C.c_size_t]),
     "arx_group_get_stats": (C.c_int, [_P, C.POINTER(ArxStats)]),

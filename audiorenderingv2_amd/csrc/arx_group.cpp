@@ -589,6 +589,90 @@ arx_status arx_group_convolute_device(arx_group* g, const float* const* d_in, si
     return ARX_OK;
 }
 
+arx_status arx_group_convolute_audio_file(arx_group* g, const float* h_in, size_t in_bytes, float* h_out_left,
+                                          float* h_out_right, double* convolute_ms, double* process_ms) {
+    if (!g || g->members.empty()) return fail(ARX_ERR_INVALID_ARGUMENT, "group is NULL or empty");
+    const size_t n = in_bytes / sizeof(float);  // AudioRenderer.cpp:689: bytes / sizeof(float)
+    if (n > 0 && (!h_in || !h_out_left || !h_out_right)) return fail(ARX_ERR_INVALID_ARGUMENT, "NULL buffer");
+    arx_renderer* r0 = g->members[0];
+    // one rank, or a plan that does not shard: the whole file on this process's first member
+    if (g->n_ranks == 1 || !conv_shards(r0))
+        return arx_convolute_audio_file(r0, h_in, in_bytes, h_out_left, h_out_right, convolute_ms, process_ms);
+    struct Events {  // per member: the call's window on its stream; destroyed on every return below
+        std::vector<std::pair<int32_t, hipEvent_t>> e;
+        ~Events() {
+            for (auto& d : e) {
+                hipSetDevice(d.first);
+                hipEventDestroy(d.second);
+            }
+        }
+    } ev;
+    const int32_t sr = r0->cfg.sample_rate;
+    std::vector<uint64_t> conv_slot(g->members.size(), 0);
+    for (size_t i = 0; i < g->members.size(); ++i) {
+        arx_renderer* r = g->members[i];
+        const int32_t rank = g->rank0 + (int32_t)i;
+        ARX_HIP(hipSetDevice(r->cfg.device));
+        if (const arx_status w = fif_wait_conv(r); w != ARX_OK) return w;  // the staging buffers below
+        hipEvent_t p0 = nullptr, p1 = nullptr;
+        ARX_HIP(hipEventCreate(&p0));
+        ev.e.emplace_back(r->cfg.device, p0);
+        ARX_HIP(hipEventCreate(&p1));
+        ev.e.emplace_back(r->cfg.device, p1);
+        ARX_HIP(hipEventRecord(p0, r->stream));
+        if (n > r->conv_cap) {
+            hipFree(r->d_conv_in);
+            hipFree(r->d_conv_out);
+            r->d_conv_in = r->d_conv_out = nullptr;
+            r->conv_cap = 0;
+            ARX_HIP(hipMalloc(&r->d_conv_in, n * sizeof(float)));
+            ARX_HIP(hipMalloc(&r->d_conv_out, 2 * n * sizeof(float)));
+            r->conv_cap = n;
+        }
+        uint64_t pb = 0, pe = 0, b = 0, e = 0;
+        conv_pairs_of(sr, n, rank, g->n_ranks, &pb, &pe);
+        arx_group_conv_shard(sr, n, rank, g->n_ranks, &b, &e);
+        // only the input this shard reads: its block pairs and the seam pair before them
+        const uint64_t S = n / (uint64_t)sr;
+        const uint64_t in_lo = std::min<uint64_t>(pb > 0 ? 2 * (pb - 1) * (uint64_t)sr : 0, n);
+        const uint64_t in_hi = (pe > pb && S > 0) ? std::min<uint64_t>(2 * pe * (uint64_t)sr, n) : in_lo;
+        if (in_hi > in_lo)
+            ARX_HIP(hipMemcpyAsync(r->d_conv_in + in_lo, h_in + in_lo, (in_hi - in_lo) * sizeof(float),
+                                   hipMemcpyHostToDevice, r->stream));
+        const bool timing = r->timing;
+        r->timing = timing || convolute_ms != nullptr;  // the convolution's own window when asked for
+        arx_status st = convolute_pairs(r, r->d_conv_in, n, r->d_conv_out, r->d_conv_out + n, (int64_t)pb, (int64_t)pe);
+        conv_slot[i] = r->conv_launches;
+        r->timing = timing;
+        if (st != ARX_OK) return st;
+        if (e > b) {  // this rank's output frames back into the caller's buffers
+            ARX_HIP(hipMemcpyAsync(h_out_left + b, r->d_conv_out + b, (e - b) * sizeof(float), hipMemcpyDeviceToHost,
+                                   r->stream));
+            ARX_HIP(hipMemcpyAsync(h_out_right + b, r->d_conv_out + n + b, (e - b) * sizeof(float),
+                                   hipMemcpyDeviceToHost, r->stream));
+        }
+        ARX_HIP(hipEventRecord(p1, r->stream));
+    }
+    double conv = 0.0, proc = 0.0;
+    for (size_t i = 0; i < g->members.size(); ++i) {
+        arx_renderer* r = g->members[i];
+        ARX_HIP(hipSetDevice(r->cfg.device));
+        hipEvent_t p0 = ev.e[2 * i].second, p1 = ev.e[2 * i + 1].second;
+        ARX_HIP(hipEventSynchronize(p1));
+        float ms = 0.f;
+        ARX_HIP(hipEventElapsedTime(&ms, p0, p1));
+        proc = std::max(proc, (double)ms);
+        if (convolute_ms && conv_slot[i] > 0) {
+            const int slot = (int)((conv_slot[i] - 1) % arx_renderer::kTraceRing);
+            ARX_HIP(hipEventElapsedTime(&ms, r->cev0[slot], r->cev1[slot]));
+            conv = std::max(conv, (double)ms);
+        }
+    }
+    if (convolute_ms) *convolute_ms = conv;
+    if (process_ms) *process_ms = proc;
+    return ARX_OK;
+}
+
 int32_t arx_group_conv_sharded(arx_group* g) {
     if (!g || g->members.empty()) return -1;
     return conv_shards(g->members[0]) ? 1 : 0;

@@ -538,6 +538,18 @@ class RenderGroup:
         P = C.c_void_p * k
         check(lib().arx_group_convolute_device(self._g, P(*d_in), int(n_frames), P(*d_out_left), P(*d_out_right)))
 
+    def convoluteAudioFile(self, samples: np.ndarray) -> tuple[np.ndarray, np.ndarray, float, float]:
+        """AudioRenderer::convoluteAudioFile over the group (arx_group_convolute_audio_file): host in,
+        host out, every GPU of this process convolving its time-block shard; bit-identical to one
+        renderer's convoluteAudioFile.  Returns (L, R, convolute_ms, process_ms)."""
+        x = np.ascontiguousarray(samples, np.float32)
+        L = np.zeros_like(x)
+        R = np.zeros_like(x)
+        cms, pms = C.c_double(), C.c_double()
+        check(lib().arx_group_convolute_audio_file(self._g, fptr(x), x.nbytes, fptr(L), fptr(R), C.byref(cms),
+                                                   C.byref(pms)))
+        return L, R, cms.value, pms.value
+
     def conv_shard(self, n_frames: int, rank: int, n_ranks: int | None = None) -> tuple[int, int]:
         """Output frames [begin, end) rank `rank` owns in a sharded convolution (arx_group_conv_shard)."""
         b, e = C.c_uint64(), C.c_uint64()

@@ -297,6 +297,17 @@ arx_status arx_group_allreduce_times(arx_group* g, int32_t member, double* ms, s
  * arx_convolute_device; arx_conv_times per member time each shard. */
 arx_status arx_group_convolute_device(arx_group* g, const float* const* d_in, size_t n_frames,
                                       float* const* d_out_left, float* const* d_out_right);
+/* AudioRenderer::convoluteAudioFile over the group (AudioRenderer.cpp:663-750: host buffers, sizes in
+ * BYTES, reference normalisation): every member of this process convolves its time-block shard
+ * (arx_group_convolute_device), copying in only the input its pairs read and copying back only the
+ * frames it owns, so in a group of one process over several GPUs h_out_left / h_out_right receive
+ * the whole convolved file -- bit-identical to arx_convolute_audio_file -- with the work spread over
+ * the GPUs.  On the one-GPU-per-process path each process fills its own ranks' frames (the caller
+ * gathers).  One rank, or a plan that does not shard: arx_convolute_audio_file on member 0.
+ * convolute_ms = the longest member's convolution window, process_ms = the longest member's whole
+ * call window (copies included); synchronising. */
+arx_status arx_group_convolute_audio_file(arx_group* g, const float* h_in, size_t in_bytes, float* h_out_left,
+                                          float* h_out_right, double* convolute_ms, double* process_ms);
 /* The output frames [begin, end) rank `rank` of n_ranks owns in a sharded convolution of n_frames at
  * sample_rate (host only; ranges of the ranks tile [0, n_frames)). */
 void arx_group_conv_shard(int32_t sample_rate, uint64_t n_frames, int32_t rank, int32_t n_ranks, uint64_t* begin,

@@ -195,14 +195,15 @@ class AudioRenderer {
         write_ir_ = false;
     }
 
-    // :31 -- sizes in bytes, host buffers owned by the caller (convolved on the first GPU); with
-    // the write-output flag set, the result is dumped once to output_convolute_{left,right}.txt
-    // and the flag cleared (AudioRenderer.cpp:720-744)
+    // :31 -- sizes in bytes, host buffers owned by the caller (on several GPUs, each convolves its
+    // time-block shard: arx_group_convolute_audio_file, bit-identical to one GPU); with the
+    // write-output flag set, the result is dumped once to output_convolute_{left,right}.txt and the
+    // flag cleared (AudioRenderer.cpp:720-744)
     void convoluteAudioFile(float* h_inputBuffer, size_t h_inputBufferSize, float* h_outputBuffer_left,
                             float* h_outputBuffer_right, double* convolute_time = nullptr,
                             double* convolute_process_time = nullptr) {
-        check(arx_convolute_audio_file(h_, h_inputBuffer, h_inputBufferSize, h_outputBuffer_left, h_outputBuffer_right,
-                                       convolute_time, convolute_process_time));
+        check(arx_group_convolute_audio_file(g_, h_inputBuffer, h_inputBufferSize, h_outputBuffer_left,
+                                             h_outputBuffer_right, convolute_time, convolute_process_time));
         if (!write_output_) return;
         const size_t n = h_inputBufferSize / sizeof(float);
         check(arx_write_float_lines("output_convolute_left.txt", h_outputBuffer_left, n));

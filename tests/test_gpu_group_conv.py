@@ -160,3 +160,24 @@ def test_allreduce_times_forced_one_rank(conference):
     assert t.size == 5 and np.all(t > 0) and np.all(t < 50.0)
     assert g.debug_collectives()["histogram_allreduce"] == 5
     g.close()
+
+
+@pytest.mark.parametrize("devices,sr,audio", [([0] * 3, 48000, "clapper"), ([0] * 5, 16000, "experimento"),
+                                              ([0], 48000, "clapper")])
+def test_group_convolute_audio_file_equals_one_renderer(conference, devices, sr, audio):
+    """arx_group_convolute_audio_file (the C++ shim's convoluteAudioFile on a group): host buffers in
+    and out, each member convolving its shard; bit-identical to one renderer's convoluteAudioFile,
+    for the reference's own recordings and for files shorter than a block or with a ragged tail."""
+    x, xsr = reference_audio(audio)
+    assert xsr == sr
+    s = RenderSettings(rays=(100, 100, 4), sample_rate=sr, base_power=3.62, max_bounces=8)
+    g = rendered_group(conference, s, devices)
+    rng = np.random.default_rng(4)
+    for sig in (x, x[: sr // 2], x[: 3 * sr + 17], rng.standard_normal(6 * sr).astype(np.float32)):
+        g.render()  # a new IR: both sides make the spectra with their first convolution
+        L, R, cms, pms = g.convoluteAudioFile(sig)
+        ref = one_gpu_conv(g.get_ir(), sr, sig)
+        assert np.array_equal(L.view(np.uint32), ref[0].view(np.uint32))
+        assert np.array_equal(R.view(np.uint32), ref[1].view(np.uint32))
+        assert pms > 0 and cms > 0
+    g.close()
