@@ -164,3 +164,42 @@ def test_frames_in_flight_refuses_a_callers_stream_or_histogram():
         r.set_stream(r.get_stream())  # allowed again with one frame in flight
     finally:
         r.close()
+
+
+def test_sharded_group_convolution_two_frames_in_flight(conference, audio):
+    """The time-block sharded convolution (arx_group_convolute_device) of an oversubscribed group with
+    two frames in flight: every frame's output frames, assembled from the ranks' shards, equal the
+    same loop's with one frame in flight."""
+    n = audio.size
+    results = {}
+    for fif in (1, 2):
+        g = RenderGroup(RenderSettings(**S), devices=[0, 0, 0], scene=conference, receiver=receiver_local())
+        g.set_frames_in_flight(fif)
+        x = [DeviceBuffer.from_numpy(0, audio) for _ in range(3)]
+        outs = []
+        for lst, yaw, em, seed in FRAMES:
+            bufs = [(DeviceBuffer(0, 4 * n), DeviceBuffer(0, 4 * n)) for _ in range(3)]
+            g.setEmitterPosInOptix(em)
+            g.setSphereCenterInOptix(lst, yaw)
+            g.set_seed(seed)
+            g.render(timed=False)
+            g.convolute_device([b.ptr for b in x], n, [b[0].ptr for b in bufs], [b[1].ptr for b in bufs])
+            outs.append(bufs)
+        g.synchronize()
+        frames = []
+        for bufs in outs:
+            L, R = np.zeros(n, np.float32), np.zeros(n, np.float32)
+            for rank, (bl, br) in enumerate(bufs):
+                b, e = g.conv_shard(n, rank)
+                L[b:e] = bl.to_numpy(np.float32, n)[b:e]
+                R[b:e] = br.to_numpy(np.float32, n)[b:e]
+                bl.close()
+                br.close()
+            frames.append((L, R))
+        for b in x:
+            b.close()
+        g.close()
+        results[fif] = frames
+    assert any(f[0].any() for f in results[1])
+    for (a, b), (c, d) in zip(results[1], results[2]):
+        assert np.array_equal(bits(a), bits(c)) and np.array_equal(bits(b), bits(d))
