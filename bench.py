@@ -86,13 +86,15 @@ HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md: measured-achievable HBM read
 
 
 # ----------------------------------------------------------------------------- rank plumbing ---
-def plan_ranks(gpus: int, env: dict, process_group: bool = False) -> dict:
+def plan_ranks(gpus: int, env: dict, process_group: bool = False, oversubscribe: bool = False) -> dict:
     """--gpus N and the launcher's environment -> how this process takes part.
 
     mode "local": this process drives devices 0..N-1 itself (one native group, ncclCommInitAll);
     mode "rank": torch.distributed.run started one process per GPU (WORLD_SIZE > 1, or
     --process-group at one rank): this process is rank RANK of WORLD_SIZE on device LOCAL_RANK
-    (ncclCommInitRank).  `world` is the GPU count of the whole job either way."""
+    (ncclCommInitRank).  `world` is the GPU count of the whole job either way.  oversubscribe (tests
+    only): mode "local" with device 0 listed N times -- the N-rank job's shards, sharded convolution
+    and bookkeeping on one GPU (its histograms summed on the device, no RCCL)."""
     if gpus < 1:
         raise ValueError(f"--gpus must be >= 1 (got {gpus})")
     world = int(env.get("WORLD_SIZE", "1"))
@@ -104,6 +106,8 @@ def plan_ranks(gpus: int, env: dict, process_group: bool = False) -> dict:
         if not (0 <= rank < world) or local < 0:
             raise ValueError(f"bad RANK={rank} / LOCAL_RANK={local} for WORLD_SIZE={world}")
         return {"mode": "rank", "world": world, "rank": rank, "devices": [local], "local_gpus_needed": local + 1}
+    if oversubscribe:
+        return {"mode": "local", "world": gpus, "rank": 0, "devices": [0] * gpus, "local_gpus_needed": 1}
     return {"mode": "local", "world": gpus, "rank": 0, "devices": list(range(gpus)), "local_gpus_needed": gpus}
 
 
@@ -531,6 +535,9 @@ def main(argv=None) -> int:
     ap.add_argument("--watchdog-s", type=float, default=None,
                     help="no progress for this long -> one JSON line {\"status\": \"hang\", ...} and exit 3 "
                          "(default: 180 s through the pre-roll, then max(30 s, 50 x the pre-roll step))")
+    ap.add_argument("--debug-oversubscribe", action="store_true",
+                    help="tests only: --gpus N as N ranks on device 0 (one process, an oversubscribed group: the "
+                         "N-rank job's shards, sharded convolution and accounting rehearsed on one GPU)")
     ap.add_argument("--debug-hang-at-step", type=int, default=-1,
                     help="tests only: stall the host inside timed step K (a stand-in for a GPU wait that never "
                          "returns), so the watchdog fires")
@@ -551,7 +558,7 @@ def main(argv=None) -> int:
                          "torch.distributed.run path on a one-GPU box")
     args = ap.parse_args(argv)
     try:
-        plan = plan_ranks(args.gpus, os.environ, args.process_group)
+        plan = plan_ranks(args.gpus, os.environ, args.process_group, args.debug_oversubscribe)
     except ValueError as e:
         raise SystemExit(f"bench.py: {e}")
 
@@ -878,12 +885,16 @@ def main(argv=None) -> int:
             "conv_frames_owned_rank0": [int(own[0][0]), int(own[0][1])],
             "frames_in_flight": args.frames_in_flight,
             "parallelism": (f"ray-shard x{world}, "
-                            + ("native RCCL int64 IR all-reduce per step" if world > 1 else
+                            + ("REHEARSAL (--debug-oversubscribe): the ranks' histograms summed on device 0, no RCCL"
+                               if args.debug_oversubscribe else
+                               "native RCCL int64 IR all-reduce per step" if world > 1 else
                                "one rank: the group's RCCL communicator exists but arx_group_render skips its no-op "
                                "IR all-reduce (arx_group.cpp; tests/test_gpu_collectives.py forces it on one GPU)")
                             + " (arx_group: "
                             + ("one process, ncclCommInitAll over devices " + ",".join(map(str, plan["devices"]))
-                               if plan["mode"] == "local" else f"one process per GPU, ncclCommInitRank, rank {rank}")
+                               if plan["mode"] == "local" and not args.debug_oversubscribe else
+                               "one process, device 0 listed " + str(world) + " times" if args.debug_oversubscribe
+                               else f"one process per GPU, ncclCommInitRank, rank {rank}")
                             + ")"),
         },
         "runtime": runtime_info(),

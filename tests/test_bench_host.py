@@ -151,3 +151,8 @@ def test_watchdog_fires_once_without_progress_and_not_while_beating():
     d = json.loads(out.getvalue())
     assert d["status"] == "hang" and d["phase"] == "moving_listener" and d["rank"] == 2 and d["world"] == 8
     assert d["steps_done"] == 12 and d["frames_in_flight"] == 1 and d["seconds_since_progress"] >= 0.2
+
+
+def test_oversubscribed_rehearsal_plan():
+    p = bench.plan_ranks(4, {}, oversubscribe=True)
+    assert p == {"mode": "local", "world": 4, "rank": 0, "devices": [0, 0, 0, 0], "local_gpus_needed": 1}

@@ -138,3 +138,26 @@ def test_bench_forced_collectives_time_the_allreduce():
     assert ar is not None and 0 < ar < 50, d["phases_allreduce_why"]
     ml = d["moving_listener"]
     assert ml["allreduce_p50_ms"] > 0 and "measured" in ml["allreduce_source"]
+
+
+def test_bench_n_rank_bookkeeping_rehearsed_on_one_gpu():
+    """bench.py --gpus 3 --debug-oversubscribe: the 3-rank job on device 0 (an oversubscribed group:
+    ray shards summed on the device, the file convolution time-block sharded over the 3 members).
+    The line counts the 3-rank launch's ray-bounces, each convolved frame once, one frame in flight
+    at N > 1, and says it is a rehearsal."""
+    base = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "c2", "--steps", "3", "--warmup", "1",
+            "--c5-frames", "3", "--no-cpu-baseline", "--no-streaming", "--no-reuse", "--no-host-leg"]
+    p = subprocess.run(base + ["--gpus", "3", "--debug-oversubscribe"], cwd=REPO, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    c = d["config"]
+    assert d["n_gpus"] == 3 and "REHEARSAL" in c["parallelism"] and c["frames_in_flight"] == 1
+    assert c["rays_per_gpu"] == 100_000 and 300_000 <= d["ray_bounces_per_step"] <= 8 * 300_000
+    frames = c["audio_frames"]
+    assert c["convolved_frames_per_step"] == frames and "time-block sharded over 3" in c["convolution"]
+    b, e = c["conv_frames_owned_rank0"]
+    assert b == 0 and 0 < e < frames  # rank 0 owns the first pairs only
+    assert d["roofline_convolution"]["frames_rank0"] == e - b
+    assert d["phases_ms_rank0"]["allreduce"] is None  # summed on the device: no RCCL collective
+    assert d["moving_listener"]["gpus"] == 3 and d["moving_listener"]["rays_per_gpu"] == 1_000_000 // 3
