@@ -122,7 +122,7 @@ def test_bench_watchdog_ends_a_hung_step_with_one_line():
     assert len(lines) == 1, p.stdout[:2000]
     d = json.loads(lines[0])
     assert d["status"] == "hang" and d["phase"] == "timed" and d["rank"] == 0 and d["world"] == 1
-    assert d["limit_s"] == 4.0 and d["seconds_since_progress"] > 4.0 and d["frames_in_flight"] == 3
+    assert d["limit_s"] == 4.0 and d["seconds_since_progress"] >= 4.0 and d["frames_in_flight"] == 3  # rounded to 0.01 s
 
 
 def test_bench_forced_collectives_time_the_allreduce():
