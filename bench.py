@@ -223,8 +223,10 @@ class Watchdog:
                         "world": self.world, "steps_done": self.steps_done,
                         "seconds_since_progress": round(time.monotonic() - self._last, 2),
                         "limit_s": self.limit_s, **self.info}
-            self.out.write(json.dumps(line) + "\n")
-            self.out.flush()
+            # stdout carries one line per job: rank 0's; the other ranks say it on stderr
+            out = self.out if self.rank == 0 else sys.stderr
+            out.write(json.dumps(line) + "\n")
+            out.flush()
             self.on_hang(3)
 
 

@@ -135,7 +135,7 @@ def test_watchdog_fires_once_without_progress_and_not_while_beating():
     import time
 
     out, codes = io.StringIO(), []
-    wd = bench.Watchdog(2, 8, out=out, on_hang=codes.append, poll_s=0.05)
+    wd = bench.Watchdog(0, 8, out=out, on_hang=codes.append, poll_s=0.05)
     wd.info["frames_in_flight"] = 1
     wd.arm(0.4, "timed")
     for _ in range(12):  # beats keep it quiet
@@ -149,10 +149,22 @@ def test_watchdog_fires_once_without_progress_and_not_while_beating():
     time.sleep(0.8)
     assert codes == [3]
     d = json.loads(out.getvalue())
-    assert d["status"] == "hang" and d["phase"] == "moving_listener" and d["rank"] == 2 and d["world"] == 8
+    assert d["status"] == "hang" and d["phase"] == "moving_listener" and d["rank"] == 0 and d["world"] == 8
     assert d["steps_done"] == 12 and d["frames_in_flight"] == 1 and d["seconds_since_progress"] >= 0.2
 
 
 def test_oversubscribed_rehearsal_plan():
     p = bench.plan_ranks(4, {}, oversubscribe=True)
     assert p == {"mode": "local", "world": 4, "rank": 0, "devices": [0, 0, 0, 0], "local_gpus_needed": 1}
+
+
+def test_watchdog_of_another_rank_reports_on_stderr(capsys):
+    import io
+    import time
+
+    out, codes = io.StringIO(), []
+    wd = bench.Watchdog(3, 8, out=out, on_hang=codes.append, poll_s=0.05)
+    wd.arm(0.1, "timed")
+    time.sleep(0.5)
+    assert codes == [3] and out.getvalue() == ""  # stdout keeps rank 0's line alone
+    assert '"rank": 3' in capsys.readouterr().err
