@@ -68,6 +68,38 @@ struct Tree {
     std::vector<ChildRef> kids;  // W per node
     size_t n = 0;
     std::vector<int> depth;  // node depth below the top node (0)
+    std::vector<int> parent, owner;  // parent node of each node; the node holding each triangle record's leaf
+    void set_links(size_t n_recs) {
+        parent.assign(n, -1);
+        owner.assign(n_recs, -1);
+        for (size_t i = 0; i < n; ++i)
+            for (int s = 0; s < W; ++s) {
+                const ChildRef& c = kids[(size_t)W * i + s];
+                if (c.count == 0 && c.ref >= 0 && (size_t)c.ref < n) parent[c.ref] = (int)i;
+                if (c.count > 0)
+                    for (int k = 0; k < c.count; ++k) owner[(size_t)c.ref + k] = (int)i;
+            }
+    }
+    static int code_of(const ChildRef& c) { return c.count > 0 ? -(c.ref * 16 + c.count) - 1 : c.ref; }
+    // ENTRY=k: start a bounce's query at the ancestor (depth <= k) of the node holding the record it
+    // left from, with the siblings of that ancestor's path pushed untested (deepest on top)
+    void entry_stack(int rec, int k, std::vector<int>& out) const {
+        out.clear();
+        int e = owner[(size_t)rec];
+        while (depth[(size_t)e] > k) e = parent[(size_t)e];
+        std::vector<int> sib;
+        for (int x = e; parent[(size_t)x] >= 0; x = parent[(size_t)x]) {
+            const int p = parent[(size_t)x];
+            for (int s = 0; s < W; ++s) {
+                const ChildRef& c = kids[(size_t)W * p + s];
+                if (c.count < 0) continue;
+                if (c.count == 0 && c.ref == x) continue;
+                sib.push_back(code_of(c));
+            }
+        }
+        for (auto it = sib.rbegin(); it != sib.rend(); ++it) out.push_back(*it);
+        out.push_back(e);
+    }
     void set_depths() {
         depth.assign(n, 1 << 20);
         depth[0] = 0;
@@ -101,11 +133,15 @@ static Tree from_binary(const std::vector<BvhNode>& nodes, const BvhNode& top) {
 
 
 // closest hit with near-first order; returns hit tri index or -1
-static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Stats& st, float& best) {
+static int trace(const Tree& t, const std::vector<TriRec>& tris, const Q& q, Stats& st, float& best,
+                 const std::vector<int>* start = nullptr) {
     best = 1e30f;
     int hit = -1;
     std::vector<std::pair<float, int>> stack;  // (tn, code) ; code >= 0 node, < 0 leaf
-    stack.push_back({0.0f, 0});
+    if (start && !start->empty())  // ENTRY: the untested siblings of the entry node's path, then the entry node
+        for (int c : *start) stack.push_back({0.0f, c});
+    else
+        stack.push_back({0.0f, 0});
     size_t maxs = 0;
     bool after_leaf = false, continue_culling = false;
     while (!stack.empty()) {
@@ -215,6 +251,8 @@ int main(int argc, char** argv) {
     std::printf("spatial %d alpha %g budget %g: refs %zu\n", (int)bp.spatial, bp.spatial_alpha, bp.spatial_budget, b.tris.size());
     std::printf("tris %ld  binary nodes %zu depth %d\n", n, b.nodes.size(), b.depth);
     t2.set_depths();
+    t2.set_links(b.tris.size());
+    const int entry_k = std::getenv("ENTRY") ? std::atoi(std::getenv("ENTRY")) : -1;
     {
         int md = 0;
         for (size_t i = 0; i < t2.n; ++i)
@@ -246,6 +284,7 @@ int main(int argc, char** argv) {
             float o[3] = {em[0], em[1], em[2]}, d[3] = {s * std::cos(ph), s * std::sin(ph), z};
             if (chains) orc_ray_direction(1, (uint64_t)i, d);
             const double v_before = st.visits + st.leaves;
+            std::vector<int> start;
             for (int bn = 0; bn < nb; ++bn) {
                 for (int a = 0; a < 3; ++a) {
                     q.o[a] = o[a];
@@ -253,9 +292,10 @@ int main(int argc, char** argv) {
                     q.inv[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? 1e-20f : d[a]);
                 }
                 float tt;
-                const int h = trace(*trees[k], b.tris, q, st, tt);
+                const int h = trace(*trees[k], b.tris, q, st, tt, &start);
                 ++queries;
                 if (h < 0) break;
+                if (entry_k >= 0) trees[k]->entry_stack(h, entry_k, start);
                 const TriRec& tr = b.tris[h];
                 const float e1[3] = {tr.v1[0] - tr.v0[0], tr.v1[1] - tr.v0[1], tr.v1[2] - tr.v0[2]};
                 const float e2[3] = {tr.v2[0] - tr.v0[0], tr.v2[1] - tr.v0[1], tr.v2[2] - tr.v0[2]};
