@@ -44,6 +44,7 @@ class ArxStats(C.Structure):
         ("bvh_depth", C.c_int32),
         ("tree_hash", C.c_uint64), ("trace_vgprs", C.c_int32), ("trace_waves_per_simd", C.c_int32),
         ("trace_waves_target", C.c_int32), ("trace_format", C.c_int32),
+        ("trace_grid_cus", C.c_int32),
     ]
 
 

@@ -987,6 +987,7 @@ arx_status arx_create(const arx_config* cfg, arx_renderer** out) {
     r->stats.trace_waves_per_simd = r->occ[kFmtQ16][0][1];
     r->stats.trace_waves_target = r->occ[kFmtQ16][0][2];
     r->stats.trace_format = kFmtQ16;
+    r->stats.trace_grid_cus = r->cus;
     if ((e = hipMemsetAsync(r->d_hist, 0, 2 * (size_t)r->ir_len * sizeof(unsigned long long), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_ir, 0, 2 * (size_t)r->ir_len * sizeof(float), r->stream)) != hipSuccess ||
         (e = hipMemsetAsync(r->d_counters, 0, kCounters * sizeof(unsigned long long), r->stream)) != hipSuccess ||
@@ -1286,7 +1287,19 @@ arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end
     r->stats.trace_waves_per_simd = r->occ[fmt][small][1];
     r->stats.trace_waves_target = r->occ[fmt][small][2];
     if (timed) ARX_HIP(hipEventRecord(r->tev0[slot], r->stream));
-    ARX_HIP(launch_trace(a, r->cus, r->stream, r->force_global_stack));
+    // Frames in flight: a ray-pool launch is sized for half the CUs' wave slots, so the next frame's
+    // launch runs beside it for its whole length instead of only in its tail.  A launch of 1M rays
+    // gives each lane about three rays; the last of them leave the lanes idle one by one, and a wave
+    // holds its slot until its last lane is done (C3 on the full grid: 5.87e9 queries/s at 1M rays
+    // against 7.23e9 at 10M).  Two half grids side by side: C3 2.60 -> 2.44 ms per frame (DESIGN.md
+    // section 6.3, profiles/r06/grid_ab_*.txt); more than half each makes a launch's last blocks wait
+    // for the other's (55 %: 2.9 ms).  One frame in flight keeps the full grid.
+#ifndef ARX_SHARED_GRID_PCT
+#define ARX_SHARED_GRID_PCT 50  // design experiments only (build.py --exp): other shares
+#endif
+    const int grid_cus = (r->fif >= 2 && !small) ? std::max(1, r->cus * ARX_SHARED_GRID_PCT / 100) : r->cus;
+    r->stats.trace_grid_cus = grid_cus;
+    ARX_HIP(launch_trace(a, grid_cus, r->stream, r->force_global_stack));
     if (timed) {
         ARX_HIP(hipEventRecord(r->tev1[slot], r->stream));
         ++r->trace_launches;

@@ -803,6 +803,7 @@ arx_status arx_group_get_stats(arx_group* g, arx_stats* out) {
         sum.trace_waves_per_simd = s.trace_waves_per_simd;
         sum.trace_waves_target = s.trace_waves_target;
         sum.trace_format = s.trace_format;
+        sum.trace_grid_cus = s.trace_grid_cus;
     }
     *out = sum;
     return ARX_OK;

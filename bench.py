@@ -730,6 +730,7 @@ def main(argv=None) -> int:
     timed_leg_ms = ranks.max(time.perf_counter() - t0k) / args.steps * 1e3
     trace_list = m0.trace_times(args.steps)
     assert len(trace_list) == args.steps, (len(trace_list), args.steps)
+    grid_cus_single = int(m0.stats()["trace_grid_cus"])
     trace_ms = float(np.mean(trace_list))
     # the histogram all-reduce's own window (HIP events on each member's stream around the RCCL call,
     # arx_group_allreduce_times), the slowest member, max over ranks; none at one rank unless forced
@@ -886,6 +887,9 @@ def main(argv=None) -> int:
             "convolved_frames_per_step": unique_frames,
             "conv_frames_owned_rank0": [int(own[0][0]), int(own[0][1])],
             "frames_in_flight": args.frames_in_flight,
+            # the persistent trace grid (arx_stats.trace_grid_cus): half the CUs' wave slots per launch
+            # with frames in flight, so two frames' launches run side by side; the full device with one
+            "trace_grid_cus": {"timed_steps": int(st0["trace_grid_cus"]), "kernel_times_leg": grid_cus_single},
             "parallelism": (f"ray-shard x{world}, "
                             + ("REHEARSAL (--debug-oversubscribe): the ranks' histograms summed on device 0, no RCCL"
                                if args.debug_oversubscribe else

@@ -75,6 +75,9 @@ typedef struct arx_stats {
     int32_t trace_waves_target;
     int32_t trace_format;    /* node format of the last trace launch: 0 f32 BVH2, 1 16-bit quantized BVH2,
                               * 2 4-wide compressed (CW4) */
+    int32_t trace_grid_cus;  /* CUs the last trace launch's persistent grid was sized for: the device's,
+                              * or half of them for a ray-pool launch with frames in flight (its wave
+                              * slots then hold two frames' launches side by side, arx_set_frames_in_flight) */
 } arx_stats;
 
 const char* arx_status_string(arx_status s);

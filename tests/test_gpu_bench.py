@@ -75,6 +75,9 @@ def test_bench_prints_one_contract_line():
     # C2 runs three frames in flight in the timed steps (tests/test_gpu_frames.py: bit-identical
     # results), the per-launch times from the single-frame leg beside them
     assert d["config"]["frames_in_flight"] == 3
+    # C2 is a launch without the ray pool: the full grid in the timed steps too (arx_stats.trace_grid_cus)
+    tg = d["config"]["trace_grid_cus"]
+    assert tg["timed_steps"] == tg["kernel_times_leg"] >= 2
     sf = d["single_frame"]
     assert sf["value"] > 0 and sf["ms_per_step"] > 0
     assert d["phases_ms_rank0"]["trace_kernel"] < sf["ms_per_step"]

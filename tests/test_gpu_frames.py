@@ -37,7 +37,7 @@ def bits(a):
     return np.asarray(a).view(np.uint32)
 
 
-def run_sequence(obj, members, audio, fif):
+def run_sequence(obj, members, audio, fif, rays=S["rays"]):
     """The frame loop without a synchronisation between frames; returns per-frame convolutions (own
     buffers), the shared buffers' final content, the last IR and the last frame's counters."""
     obj.set_frames_in_flight(fif)
@@ -53,7 +53,7 @@ def run_sequence(obj, members, audio, fif):
             obj.render(timed=False)
         else:
             obj.clear_histogram()
-            obj.trace_rays(0, int(np.prod(S["rays"])))
+            obj.trace_rays(0, int(np.prod(rays)))
             obj.finalize_ir()
         m = members[0]
         m.convolute_device(x.ptr, n, ol.ptr, orr.ptr)
@@ -94,6 +94,47 @@ def test_renderer_frames_in_flight_equal_one_at_a_time(conference, audio, trace_
     assert np.array_equal(bits(s2[0]), bits(o2[-1][0]))  # the shared buffers hold the last frame's
     assert np.array_equal(bits(ir1[0]), bits(ir2[0])) and np.array_equal(bits(ir1[1]), bits(ir2[1]))
     assert st1 == st2
+
+
+@pytest.mark.parametrize("frames", [2, 3])
+def test_ray_pool_launches_share_the_grid_in_flight(conference, audio, frames):
+    """Launches large enough for the ray pool (C3's shape: 600K rays here) take half the CUs' wave
+    slots each with frames in flight (arx_stats.trace_grid_cus), so two frames' launches run side by
+    side; the full grid with one.  Every output bit-identical to one frame at a time."""
+    rays = (100, 100, 60)
+    res, grid = {}, {}
+    for fif in (1, frames):
+        r = AudioRenderer(RenderSettings(**dict(S, rays=rays)), scene=conference, receiver=receiver_local())
+        try:
+            res[fif] = run_sequence(r, [r], audio, fif, rays)
+            grid[fif] = r.stats()["trace_grid_cus"]
+        finally:
+            r.close()
+    assert grid[1] >= 2 and grid[frames] == grid[1] // 2, grid
+    (o1, s1, ir1, st1), (o2, s2, ir2, st2) = res[1], res[frames]
+    assert ir1[0].any() and st1[1] > 0
+    for k, (a, b) in enumerate(zip(o1, o2)):
+        assert np.array_equal(bits(a[0]), bits(b[0])) and np.array_equal(bits(a[1]), bits(b[1])), f"frame {k}"
+    assert np.array_equal(bits(s1[0]), bits(s2[0])) and np.array_equal(bits(s1[1]), bits(s2[1]))
+    assert np.array_equal(bits(ir1[0]), bits(ir2[0])) and np.array_equal(bits(ir1[1]), bits(ir2[1]))
+    assert st1 == st2
+
+
+def test_small_launches_keep_the_full_grid_in_flight(conference):
+    """A launch without the ray pool (about a ray per lane, C2's shape) is its longest lane's chain:
+    it keeps the full grid with frames in flight."""
+    r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
+    try:
+        r.setEmitterPosInOptix(CONFERENCE_EMITTER)
+        r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
+        r.render()
+        full = r.stats()["trace_grid_cus"]
+        r.set_frames_in_flight(2)
+        r.render()
+        r.get_ir()
+        assert r.stats()["trace_grid_cus"] == full >= 2
+    finally:
+        r.close()
 
 
 def test_group_render_two_frames_in_flight_equal_one_at_a_time(conference, audio):
