@@ -976,6 +976,12 @@ def main(argv=None) -> int:
                               "build, tree and workload; PMC counters cannot be read inside this run): " + traffic_why,
             "algorithmic_bytes_per_bounce": bpb,
             "trace_launch_ms": trace_ms,
+            # the timed steps' own rate by the same convention: with frames in flight two launches
+            # run side by side on half the grid each (config.trace_grid_cus), one frame per step
+            "timed_steps_achieved": q_m0 * bpb / (elapsed / args.steps * 1e-3) / 1e9,
+            "launch_note": "trace_launch_ms / achieved / frac: one launch alone on the full grid (the kernel-times "
+                           "leg); timed_steps_achieved: the same bytes per frame over the timed steps' ms_per_step, "
+                           "where frames in flight overlap their launches",
         },
         "roofline_convolution": {
             "bound": "hbm",
