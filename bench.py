@@ -510,7 +510,7 @@ def _stdout_to_stderr():
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--preroll-s", type=float, default=0.5,
                     help="untimed steps for this long before the warmup steps: a fresh process on an idle GPU "
@@ -978,7 +978,7 @@ def main(argv=None) -> int:
             "trace_launch_ms": trace_ms,
             # the timed steps' own rate by the same convention: with frames in flight two launches
             # run side by side on half the grid each (config.trace_grid_cus), one frame per step
-            "timed_steps_achieved": q_m0 * bpb / (elapsed / args.steps * 1e-3) / 1e9,
+            "timed_steps_achieved": q_m0 * bpb / (elapsed / args.steps) / 1e9,
             "launch_note": "trace_launch_ms / achieved / frac: one launch alone on the full grid (the kernel-times "
                            "leg); timed_steps_achieved: the same bytes per frame over the timed steps' ms_per_step, "
                            "where frames in flight overlap their launches",

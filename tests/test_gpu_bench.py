@@ -35,6 +35,9 @@ def test_bench_prints_one_contract_line():
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in rf, k
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    # the timed steps' rate by the same convention (frames in flight overlap their launches)
+    tsa = d["ray_bounces_per_step"] * rf["algorithmic_bytes_per_bounce"] / (d["ms_per_step"] * 1e-3) / 1e9
+    assert abs(rf["timed_steps_achieved"] - tsa) < 1e-6 * tsa
     # the byte convention beside what binds: the counter traffic's fraction of HBM and the TD's busy
     # fraction (null when the stored profile is not of this workload / tree / kernel)
     for k in ("traffic_frac", "binding_frac", "binding_unit"):
