@@ -156,8 +156,12 @@ arx_status arx_render(arx_renderer* r, double* render_ms);
  * loop keeps the GPU full.  Results are those of one frame at a time, bit for bit: every getter,
  * convolution and IR copy refers to the last frame started, and the two frames meet only where they
  * share state (scene and receiver uploads wait for the other frame's trace; convolutions, IR
- * spectra and the caller's output buffers for its convolution).  Not with arx_set_stream or
- * arx_attach_histogram (ARX_ERR_INVALID_ARGUMENT either way round). */
+ * spectra and the caller's output buffers for its convolution).  A trace launch large enough for
+ * the ray pool is then sized for half the CUs' wave slots (arx_stats.trace_grid_cus), so two frames'
+ * launches run side by side instead of meeting only in each other's tail; a single frame
+ * (arx_set_frames_in_flight(r, 1)) is therefore faster alone, a render/convolute loop faster in
+ * total.  Not with arx_set_stream or arx_attach_histogram (ARX_ERR_INVALID_ARGUMENT either way
+ * round). */
 arx_status arx_set_frames_in_flight(arx_renderer* r, int32_t n);
 
 /* Building blocks of render() for ray-sharded multi-GPU use (no reference equivalent; the
