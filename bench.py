@@ -52,9 +52,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 WORKLOADS = {
     # configs[2]: conference, 1M rays x 16 bounces, 48 kHz IR + convolution (per GPU)
-    # fif: frames in flight on one GPU (a frame's tail overlaps the next frames' start): C3 +3 % with 2,
-    # no more with 3; C2, whose single frame fills 1.5 waves per SIMD, +62 % with 2 and +112 % with 3;
-    # the 48 ms C4 launch loses 5 % with 2 (profiles/r04/bench_*_fif*_r04p.json, bench_c4_r04m.json)
+    # fif: frames in flight on one GPU.  C3 with 2: two half-grid launches side by side, +8 % (round 6,
+    # profiles/r06/grid_ab_*.txt; +3 % on the full grid before); C2, whose single frame fills 1.5 waves
+    # per SIMD, +62 % with 2 and +112 % with 3; the 46 ms C4 launch loses 7-13 % with 2
+    # (profiles/r06/grid_ab_c4.txt; 5 % on the full grid, profiles/r04/bench_c4_r04m.json)
     "c3": dict(rays=(100, 100, 100), max_bounces=16, sample_rate=48000, audio="clapper", fif=2,
                desc="configs[2]: conference stand-in, 1M rays x 16 bounces per GPU, 48 kHz IR (96000 bins/ear), "
                     "file-mode FFT convolution of A_Clapper_Board.wav ch0 (807498 frames) per GPU"),
@@ -526,8 +527,10 @@ def main(argv=None) -> int:
     ap.add_argument("--frames-in-flight", type=int, choices=(1, 2, 3), default=None,
                     help="frames the group keeps in flight in the timed steps (arx_group_set_frames_in_flight): "
                          "with 2, step k+1's trace starts while step k finishes, and a single-frame leg is timed "
-                         "too.  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 48 ms launches lose 5 %% to "
-                         "the overlap).  Default at N > 1: 1, until a multi-GPU run of the frames-in-flight "
+                         "too; a ray-pool launch then takes half the CUs' wave slots, so two frames trace side by "
+                         "side (config.trace_grid_cus).  Default on one GPU: 3 for c2, 2 for c3, 1 for c4 (its 46 ms "
+                         "launches have little tail to hide and lose 7-13 %% on half grids, "
+                         "profiles/r06/grid_ab_c4.txt).  Default at N > 1: 1, until a multi-GPU run of the frames-in-flight "
                          "all-reduce chain is on record (each frame's all-reduce runs on its own frame stream after "
                          "the previous frame's; tests/test_gpu_collectives.py runs that chain with every "
                          "collective forced on one GPU only)")
