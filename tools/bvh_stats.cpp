@@ -100,6 +100,29 @@ struct Tree {
         for (auto it = sib.rbegin(); it != sib.rend(); ++it) out.push_back(*it);
         out.push_back(e);
     }
+    // ENTRYT=k: as ENTRY, but each sibling's box (the 16-B half of its parent that holds it) is tested
+    // against the query first and pushed only when hit; returns the boxes tested
+    int entry_stack_tested(int rec, int k, const Q& q, std::vector<int>& out) const {
+        out.clear();
+        int e = owner[(size_t)rec];
+        while (depth[(size_t)e] > k) e = parent[(size_t)e];
+        std::vector<int> sib;
+        int tested = 0;
+        for (int x = e; parent[(size_t)x] >= 0; x = parent[(size_t)x]) {
+            const int p = parent[(size_t)x];
+            for (int s = 0; s < W; ++s) {
+                const ChildRef& c = kids[(size_t)W * p + s];
+                if (c.count < 0) continue;
+                if (c.count == 0 && c.ref == x) continue;
+                ++tested;
+                float tn;
+                if (slab(c.lo, c.hi, q, 1e30f, tn)) sib.push_back(code_of(c));
+            }
+        }
+        for (auto it = sib.rbegin(); it != sib.rend(); ++it) out.push_back(*it);
+        out.push_back(e);
+        return tested;
+    }
     void set_depths() {
         depth.assign(n, 1 << 20);
         depth[0] = 0;
@@ -253,6 +276,8 @@ int main(int argc, char** argv) {
     t2.set_depths();
     t2.set_links(b.tris.size());
     const int entry_k = std::getenv("ENTRY") ? std::atoi(std::getenv("ENTRY")) : -1;
+    const int entry_t = std::getenv("ENTRYT") ? std::atoi(std::getenv("ENTRYT")) : -1;
+    double sib_tests = 0;
     {
         int md = 0;
         for (size_t i = 0; i < t2.n; ++i)
@@ -296,6 +321,7 @@ int main(int argc, char** argv) {
                 ++queries;
                 if (h < 0) break;
                 if (entry_k >= 0) trees[k]->entry_stack(h, entry_k, start);
+                const int hit_rec = h;
                 const TriRec& tr = b.tris[h];
                 const float e1[3] = {tr.v1[0] - tr.v0[0], tr.v1[1] - tr.v0[1], tr.v1[2] - tr.v0[2]};
                 const float e2[3] = {tr.v2[0] - tr.v0[0], tr.v2[1] - tr.v0[1], tr.v2[2] - tr.v0[2]};
@@ -307,6 +333,15 @@ int main(int argc, char** argv) {
                     o[a] = o[a] + tt * d[a];
                     d[a] -= dn * ng[a];
                     o[a] += 1e-3f * d[a];
+                }
+                if (entry_t >= 0) {
+                    Q qn;
+                    for (int a = 0; a < 3; ++a) {
+                        qn.o[a] = o[a];
+                        qn.d[a] = d[a];
+                        qn.inv[a] = 1.0f / (std::fabs(d[a]) < 1e-20f ? 1e-20f : d[a]);
+                    }
+                    sib_tests += trees[k]->entry_stack_tested(hit_rec, entry_t, qn, start);
                 }
             }
             if (chains) ray_visits.push_back(st.visits + st.leaves - v_before);
@@ -331,6 +366,7 @@ int main(int argc, char** argv) {
                         wave_max[wave_max.size() / 2], wave_max.back());
         }
         const double v = st.visits / queries, te = st.tests / queries, lv = st.leaves / queries;
+        if (entry_t >= 0) std::printf("ENTRYT=%d: sibling box tests per query %.2f\n", entry_t, sib_tests / queries);
         std::printf("W=%d: %ld queries  visits %.1f  leaves %.1f  tri tests %.1f  node bytes %.0f  tri bytes %.0f  "
                     "max stack %.0f\n",
                     trees[k]->W, queries, v, lv, te, v * node_bytes[k], te * 48.0, st.maxstack);
