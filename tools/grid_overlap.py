@@ -41,11 +41,16 @@ def main(trace_csv, bench_json):
         "timed_start_period_ms": (starts[-1] - starts[0]) / (len(starts) - 1) / 1e6,
         "timed_concurrency_at_midpoint": sum(conc) / len(conc),
         "single_frame_avg_duration_ms": sum((e - b) / 1e6 for b, e, _ in alone) / len(alone),
+        # the kernel-times leg (the last W + K of the single-frame launches) against the line's HIP events
+        "kernel_times_leg_avg_ms": sum((e - b) / 1e6 for b, e, _ in alone[-k:]) / k,
+        "bench_hip_events_ms": d["phases_ms_rank0"]["trace_kernel"],
+        "all_trace_launches_avg_ms": sum((e - b) / 1e6 for b, e, _ in iv) / len(iv),
         "bench_ms_per_step": d["ms_per_step"],
         "bench_value": d["value"],
         "frames_in_flight": d["config"]["frames_in_flight"],
         "trace_grid_cus": d["config"].get("trace_grid_cus"),
     }
+    out["agreement"] = out["kernel_times_leg_avg_ms"] / out["bench_hip_events_ms"] - 1.0
     json.dump(out, sys.stdout, indent=1)
 
 
