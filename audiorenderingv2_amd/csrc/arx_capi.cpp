@@ -1293,11 +1293,14 @@ arx_status arx::trace_rays(arx_renderer* r, uint64_t ray_begin, uint64_t ray_end
     // holds its slot until its last lane is done (C3 on the full grid: 5.87e9 queries/s at 1M rays
     // against 7.23e9 at 10M).  Two half grids side by side: C3 2.60 -> 2.44 ms per frame (DESIGN.md
     // section 6.3, profiles/r06/grid_ab_*.txt); more than half each makes a launch's last blocks wait
-    // for the other's (55 %: 2.9 ms).  One frame in flight keeps the full grid.
+    // for the other's (55 %: 2.9 ms).  One frame in flight keeps the full grid, and so do the traces
+    // on the renderer's one global stack (deep trees, CW4): they wait for every other frame's trace
+    // above, so they never run beside one.
 #ifndef ARX_SHARED_GRID_PCT
 #define ARX_SHARED_GRID_PCT 50  // design experiments only (build.py --exp): other shares
 #endif
-    const int grid_cus = (r->fif >= 2 && !small) ? std::max(1, r->cus * ARX_SHARED_GRID_PCT / 100) : r->cus;
+    const bool shared_grid = r->fif >= 2 && !small && !gstack && !a.wbuf;
+    const int grid_cus = shared_grid ? std::max(1, r->cus * ARX_SHARED_GRID_PCT / 100) : r->cus;
     r->stats.trace_grid_cus = grid_cus;
     ARX_HIP(launch_trace(a, grid_cus, r->stream, r->force_global_stack));
     if (timed) {

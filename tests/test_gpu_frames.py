@@ -120,11 +120,14 @@ def test_ray_pool_launches_share_the_grid_in_flight(conference, audio, frames):
     assert st1 == st2
 
 
-def test_small_launches_keep_the_full_grid_in_flight(conference):
-    """A launch without the ray pool (about a ray per lane, C2's shape) is its longest lane's chain:
-    it keeps the full grid with frames in flight."""
-    r = AudioRenderer(RenderSettings(**S), scene=conference, receiver=receiver_local())
+@pytest.mark.parametrize("rays,trace_path", [(S["rays"], 0), ((100, 100, 60), 2)])
+def test_launches_that_cannot_share_keep_the_full_grid_in_flight(conference, rays, trace_path):
+    """A launch without the ray pool (about a ray per lane, C2's shape) is its longest lane's chain, and
+    a trace on the renderer's one global stack waits for the other frames' traces: both keep the full
+    grid with frames in flight."""
+    r = AudioRenderer(RenderSettings(**dict(S, rays=rays)), scene=conference, receiver=receiver_local())
     try:
+        r.set_trace_path(trace_path)
         r.setEmitterPosInOptix(CONFERENCE_EMITTER)
         r.setSphereCenterInOptix(CONFERENCE_LISTENER, 0.0)
         r.render()
