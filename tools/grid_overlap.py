@@ -28,10 +28,9 @@ def main(trace_csv, bench_json):
     timed = seg[end - k:end]
     durs = [(e - b) / 1e6 for b, e, _ in timed]
     starts = [b for b, _, _ in timed]
-    conc = []
-    for b, e, _ in timed:  # launches running at this launch's midpoint (itself included)
-        m = (b + e) / 2
-        conc.append(sum(1 for b2, e2, _ in seg if b2 <= m < e2))
+    # launches running at once, averaged over the timed launches' span (sum of durations / span)
+    span = max(e for _, e, _ in timed) - min(b for b, _, _ in timed)
+    conc = sum(e - b for b, e, _ in timed) / span
     alone = seg[end:end + single]
     out = {
         "timed_launches": len(timed),
@@ -39,7 +38,7 @@ def main(trace_csv, bench_json):
         "single_frame_grid": sorted(set(g for _, _, g in alone)),
         "timed_avg_duration_ms": sum(durs) / len(durs),
         "timed_start_period_ms": (starts[-1] - starts[0]) / (len(starts) - 1) / 1e6,
-        "timed_concurrency_at_midpoint": sum(conc) / len(conc),
+        "timed_mean_concurrency": conc,
         "single_frame_avg_duration_ms": sum((e - b) / 1e6 for b, e, _ in alone) / len(alone),
         # the kernel-times leg (the last W + K of the single-frame launches) against the line's HIP events
         "kernel_times_leg_avg_ms": sum((e - b) / 1e6 for b, e, _ in alone[-k:]) / k,
